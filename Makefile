@@ -1,0 +1,39 @@
+# Builds build/libbert.so — the drop-in for the reference's libbert.so
+# (the path examples/sample_dylib.py:17 and benchmarks/run_mteb.py:47 dlopen).
+#   make            -> build/libbert.so (HIP kernels for gfx950 + host runtime)
+#   make oracle     -> oracle/_build/liboracle.so (CPU checker, tests only)
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+BUILD := build
+SRC := embedding.cpp_amd/csrc
+INC := -Iinclude -I$(SRC)
+HOST_SRCS := gguf_io.cpp quantize.cpp quantize_model.cpp synth.cpp tokenizer.cpp runtime.cpp
+HOST_OBJS := $(addprefix $(BUILD)/obj/,$(HOST_SRCS:.cpp=.o))
+HIP_OBJS := $(BUILD)/obj/kernels.o
+CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result \
+            -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
+HIPFLAGS := -O3 -std=c++17 -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
+
+all: $(BUILD)/libbert.so
+
+$(BUILD)/obj/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/bert.h include/bert_amd.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/obj/tokenizer.o: $(SRC)/unicode_tables.inc
+
+$(BUILD)/obj/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.h
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/libbert.so: $(HOST_OBJS) $(HIP_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD)
+
+.PHONY: all oracle clean

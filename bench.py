@@ -1,0 +1,305 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's headline metric on MI355X.
+
+Metric: embeddings/sec at seq_len=128, batch=1024 (all-MiniLM-L6-v2 Q4_0 shape,
+synthetic deterministic weights: no checkpoints offline), plus cosine
+similarity vs the ggml-semantics CPU oracle.  One "step" = one pass of the
+embedding path (bert_amd_eval_device: embed+LN, 6 x {QKV, attention, O+LN,
+FFN-up+GELU, FFN-down+LN}, mean-pool+L2) over one batch of 1024 sentences x 128
+tokens already resident in HBM.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+one process per GPU, each rank evaluates its own 1024 sentences (weak scaling;
+sentences are independent, reference bert.cpp:1065, so there is no data-path
+collective); RCCL is used only for the barrier and the max-over-ranks time.
+
+Prints exactly one JSON line on rank 0 (everything else goes to stderr).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "embedding.cpp_amd"))
+
+import bertlib  # noqa: E402
+
+SEED = 20250117
+METRIC = "embeddings/sec at seq_len=128 batch=1024; cosine-sim vs ggml CPU ref"
+PEAK_FP16_TFLOPS = 2516.6  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP32_MFMA_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def splitmix_tokens(first_index: int, n_sent: int, seq: int, n_vocab: int) -> np.ndarray:
+    """Sentence s: [101, r_1..r_{seq-2}, 102], r uniform in [1000, V) from
+    splitmix64(SEED + s) — identical to tests/golden/make_golden.py:sentence."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        st = (np.uint64(SEED) + np.arange(first_index, first_index + n_sent, dtype=np.uint64))
+        out = np.empty((n_sent, seq), np.int64)
+        out[:, 0] = 101
+        out[:, -1] = 102
+        for j in range(1, seq - 1):
+            st = (st + np.uint64(0x9E3779B97F4A7C15)) & M
+            z = st
+            z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M
+            z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M
+            z = z ^ (z >> np.uint64(31))
+            out[:, j] = (np.uint64(1000) + z % np.uint64(n_vocab - 1000)).astype(np.int64)
+    return out.astype(np.int32)
+
+
+def shard(rank: int, batch: int) -> int:
+    """First global sentence index of this rank's batch (weak scaling: rank r
+    owns sentences [r*batch, (r+1)*batch))."""
+    return rank * batch
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
+    E, I = hp["n_embd"], hp["n_intermediate"]
+    M = B * N
+    return {
+        "gemm_qkv": 2.0 * M * E * 3 * E,
+        "gemm_o_ln": 2.0 * M * E * E,
+        "gemm_up_gelu": 2.0 * M * E * I,
+        "gemm_down_ln": 2.0 * M * I * E,
+        "attention": 4.0 * B * N * N * E,
+    }.get(name, 0.0)
+
+
+def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
+    """Algorithmic HBM bytes per launch (each operand read once, each output written once)."""
+    E, I, L = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
+    M = B * N
+    act = {"q4_0": 1 + 2 / 32, "q4_1": 1 + 4 / 32, "f16": 2, "f32": 4}[ftype]  # bytes/elem of GEMM inputs
+    wb = {"q4_0": 18 / 32, "q4_1": 20 / 32, "f16": 2, "f32": 4}[ftype]
+    return {
+        "gemm_qkv": M * E * act + 3 * E * E * wb + M * 3 * E * 4,
+        "gemm_o_ln": M * E * act + E * E * wb + 2 * M * E * 4 + M * E * act,
+        "gemm_up_gelu": M * E * act + E * I * wb + M * I * act,
+        "gemm_down_ln": M * I * act + E * I * wb + 2 * M * E * 4 + M * E * act,
+        "attention": M * 3 * E * 4 + M * E * act,
+        "embed_ln": M * 4 + M * E * (4 + act) + M * E * 3 * wb,
+        "pool_l2": M * E * 4 + B * E * 4,
+    }.get(name, 0.0) if L else 0.0
+
+
+def pmc_traffic(csv_path: str, kernel_substr: str):
+    """Average corrected HBM bytes per dispatch of one kernel from a rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE counter CSV (gfx950: FETCH_SIZE counts half the
+    bytes of a wide coalesced read — MI355X_MICROARCH.md §HBM — so it is doubled;
+    both counters are in KB)."""
+    import csv
+    vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+    paths = csv_path.split(",")
+    for p in paths:
+        if not os.path.exists(p):
+            continue
+        with open(p) as f:
+            for row in csv.DictReader(f):
+                name = row.get("Kernel_Name", "")
+                cn = row.get("Counter_Name", "")
+                if kernel_substr in name and cn in vals:
+                    vals[cn].append(float(row.get("Counter_Value", 0)))
+    if not vals["FETCH_SIZE"] or not vals["WRITE_SIZE"]:
+        return None
+    return (2.0 * np.mean(vals["FETCH_SIZE"]) + np.mean(vals["WRITE_SIZE"])) * 1024.0
+
+
+# name fragments of the dominant kernels' mangled symbols (for PMC CSV lookup)
+KERNEL_SYMBOL = {
+    "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "gemm_kernel<2, 1,",
+    "gemm_down_ln": "gemm_kernel<2, 2,", "attention": "attention_kernel", "embed_ln": "embed_ln_kernel",
+    "pool_l2": "pool_l2_kernel",
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--shape", default="minilm", choices=list(bertlib.SHAPES))
+    ap.add_argument("--ftype", default="q4_0", choices=list(bertlib.FTYPES))
+    ap.add_argument("--w-std", type=float, default=0.05)
+    ap.add_argument("--model-dir", default=os.environ.get("BERT_AMD_MODEL_DIR", "/tmp/bert_amd_models"))
+    ap.add_argument("--cpu-sample", type=int, default=64, help="sentences for the CPU oracle baseline (0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--pmc-csv", default=os.environ.get("BENCH_PMC_CSV", ""))
+    args = ap.parse_args()
+
+    import torch
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    hp = bertlib.SHAPES[args.shape]
+    os.makedirs(args.model_dir, exist_ok=True)
+    path = os.path.join(args.model_dir, f"{args.shape}_{args.ftype}_s{SEED}_w{args.w_std:g}.gguf")
+    if local_rank == 0 and not os.path.exists(path):
+        tmp = f"{path}.tmp{os.getpid()}"
+        bertlib.synth_model(tmp, args.shape, args.ftype, seed=SEED, w_std=args.w_std)
+        os.replace(tmp, path)
+    barrier()
+    while not os.path.exists(path):  # other nodes' local rank 0 (single node: already there)
+        time.sleep(0.1)
+
+    model = bertlib.BertModel(path, devices=[local_rank])
+    B, N = args.batch, args.seq
+    first = shard(rank, B)
+    toks = splitmix_tokens(first, B, N, hp["n_vocab"])
+    offs = (np.arange(B + 1, dtype=np.int64) * N).astype(np.int32)
+    d_tok = torch.from_numpy(toks.ravel()).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_out = torch.empty(B, hp["n_embd"], dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        model.eval_device(d_tok.data_ptr(), d_off.data_ptr(), offs, B, d_out.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    t1 = time.perf_counter()
+    dt = max_over_ranks(t1 - t0, dev)
+    value = world * B * args.steps / dt
+    ms_per_step = dt / args.steps * 1e3
+    out = d_out.cpu().numpy()
+
+    # per-kernel durations: HIP events recorded by the library around every launch,
+    # on the launch stream, in a separate pass of profile-steps steps right after
+    # the timed region (the timed region itself carries no events)
+    model.profile(True)
+    for _ in range(args.profile_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    prof = model.profile_read()
+    model.profile(False)
+    kern = {}
+    for name, (ms, cnt) in prof.items():
+        fl = kernel_flops(name, B, N, hp)
+        by = kernel_bytes(name, B, N, hp, args.ftype)
+        avg_s = ms / max(cnt, 1) / 1e3
+        kern[name] = dict(avg_us=round(avg_s * 1e6, 2), launches_per_step=cnt // max(args.profile_steps, 1),
+                          share=round(ms / max(sum(v[0] for v in prof.values()), 1e-9), 4),
+                          tflops=round(fl / avg_s / 1e12, 1) if fl else None,
+                          gbs=round(by / avg_s / 1e9, 1) if by else None)
+    dominant = max(prof, key=lambda k: prof[k][0]) if prof else None
+
+    roofline = None
+    if dominant:
+        avg_s = prof[dominant][0] / prof[dominant][1] / 1e3
+        fl = kernel_flops(dominant, B, N, hp)
+        if fl:
+            peak = PEAK_FP32_MFMA_TFLOPS if (dominant == "attention" or args.ftype == "f32") else PEAK_FP16_TFLOPS
+            ach = fl / avg_s / 1e12
+            roofline = dict(kernel=dominant, bound="mfma", achieved=round(ach, 1), peak=peak, unit="TFLOP/s",
+                            frac=round(ach / peak, 4), flops_per_launch=fl)
+        else:
+            by = kernel_bytes(dominant, B, N, hp, args.ftype)
+            ach = by / avg_s / 1e9
+            roofline = dict(kernel=dominant, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                            frac=round(ach / PEAK_HBM_GBS, 4), bytes_per_launch=by)
+        traffic = pmc_traffic(args.pmc_csv, KERNEL_SYMBOL.get(dominant, dominant)) if args.pmc_csv else None
+        roofline["traffic"] = traffic
+        roofline["algorithmic_bytes_per_launch"] = kernel_bytes(dominant, B, N, hp, args.ftype)
+
+    # whole-path MFMA fraction: F(N) = L(8NE^2 + 4NEI + 4N^2E) per sentence
+    E, I, L = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
+    f_sent = L * (8 * N * E * E + 4 * N * E * I + 4 * N * N * E)
+    path_frac = f_sent * value / (world * PEAK_FP16_TFLOPS * 1e12)
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # CPU checker + baseline only (never the measured path)
+        threads = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        S = min(args.cpu_sample, B)
+        orc = oracle.Oracle(path)
+        sample = [toks[i].tolist() for i in range(S)]
+        orc.eval_batch(sample[:1], threads)  # warm-up (page-in of the model file)
+        c0 = time.perf_counter()
+        ref = orc.eval_batch(sample, threads)
+        c1 = time.perf_counter()
+        cpu = dict(value=round(S / (c1 - c0), 3), unit="embeddings/s", cores=threads, kind="port",
+                   sample=f"first {S} of the {B} sentences (seq_len {N}), oracle/bert_oracle.c "
+                          f"(ggml-semantics C restatement, one sentence at a time, {threads} OpenMP threads, "
+                          f"-O3 -march=x86-64-v3)", seconds=round(c1 - c0, 2))
+        a = out[:S].astype(np.float64)
+        c = (a * ref).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(ref, axis=1)
+        parity = dict(cos_min=float(c.min()), cos_mean=float(c.mean()), n=S,
+                      max_abs=float(np.abs(out[:S] - ref).max()))
+
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": round(value, 1), "unit": "embeddings/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+            "dtype_note": f"{args.ftype} weights dequantised to fp16 in registers, "
+                          f"{'Q8 activations dequantised to fp16, ' if args.ftype.startswith('q') else ''}"
+                          "fp16 MFMA with f32 accumulate; attention f32 MFMA; LN/softmax sums f64",
+            "data": "synthetic (deterministic splitmix64 token ids and weights; no checkpoints offline)",
+            "config": {"workload": f"{args.shape} {args.ftype} batch={B} seq_len={N} per GPU",
+                       "model": f"all-MiniLM-L6-v2 shape ({args.shape}), synthetic weights" if args.shape == "minilm"
+                       else f"{args.shape} shape, synthetic weights",
+                       "global_batch": B * world, "seq_len": N, "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "pipeline_mfma_frac": round(path_frac, 4),
+            "kernels": kern,
+            "cosine_vs_oracle": parity,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    model.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,93 @@
+// kernels.h — launch interface between the host runtime and the HIP kernels.
+//
+// One fixed pipeline replaces the reference's per-sentence ggml graph
+// (reference bert.cpp:845-1012 built, :1080 computed, once per sentence):
+//
+//   embed_ln  : get_rows x3 + add + add + norm/mul/add   (bert.cpp:880-898)
+//   per layer:
+//     gemm<QKV>   : Q|K|V = b + W.x for all three heads-blocks  (:905-926)
+//     attention   : K.Q, scale, soft_max, V^T.P, permute/cpy   (:928-942)
+//     gemm<LN>    : LN(b_o + W_o.ctx + x)                       (:944-962)
+//     gemm<GELU>  : gelu(b_i + W_i.h)                           (:965-971)
+//     gemm<LN>    : LN(h + b_o2 + W_o2.u)                       (:973-992)
+//   pool_l2   : mean pool as matvec, sum of squares, sqrt, 1/len, scale (:995-1006)
+//
+// Sentences of different lengths are packed row-wise ("ragged batch"): rows
+// [offsets[s], offsets[s+1]) belong to sentence s; attention never mixes
+// sentences, so per-sentence semantics equal the reference's one-at-a-time loop.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bertamd {
+
+// weight type of the 2-D matrices; the activation format feeding a GEMM
+// follows it exactly like ggml's vec_dot_type:
+//   W_F32 -> f32, W_F16 -> fp16 (RNE), W_Q4_0 -> Q8_0 (int8 + fp16 d),
+//   W_Q4_1 -> Q8_1 (int8 + f32 d)
+enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3 };
+
+struct ActPtr {
+    void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K]
+    void *d = nullptr;  // per-32-block scale [M][K/32]: fp16 (Q8_0) | f32 (Q8_1)
+};
+
+// Weights repacked at load time into MFMA fragment order:
+//   per (16-row n-tile, 32-wide k-block) one 64-lane fragment.
+//   Q4_x: q = u32 [N/16][K/32][64] (8 nibbles per lane), d (and m) = fp16 [N/16][K/32][16]
+//   F16 : q = fp16 [N/16][K/32][64][8]
+//   F32 : q = f32  [N/16][K/32][64][8]
+struct WPtr {
+    const void *q = nullptr;
+    const void *d = nullptr;
+    const void *m = nullptr;
+};
+
+enum Epi : int { EPI_BIAS_F32 = 0, EPI_GELU_ACT = 1, EPI_LN = 2 };
+
+struct GemmArgs {
+    ActPtr A;              // [Mpad][K] in the activation format of wtype
+    int K = 0;
+    WPtr W;                // [N][K] repacked
+    int N = 0;
+    const float *bias = nullptr;   // [N]
+    float *out_f32 = nullptr;      // EPI_BIAS_F32: [Mpad][N]
+    ActPtr out_act;                // EPI_GELU_ACT: [Mpad][N]; EPI_LN: [Mpad][N]
+    float *X = nullptr;            // EPI_LN: residual in / LN out, f32 [Mpad][N]
+    const float *ln_w = nullptr, *ln_b = nullptr;
+    float eps = 0.f;
+    const uint16_t *gelu_tab = nullptr;  // fp16 -> fp16 table (ggml_init, host-built)
+};
+
+struct EmbedArgs {
+    const int32_t *tokens = nullptr;   // [M] packed
+    const int32_t *offsets = nullptr;  // [n_seqs+1]
+    int n_seqs = 0, M = 0, E = 0, n_vocab = 0, n_pos = 0;
+    const void *word = nullptr, *pos = nullptr, *type = nullptr;  // ggml row format of `ttype`
+    int word_t = 0, pos_t = 0, type_t = 0;
+    const float *ln_w = nullptr, *ln_b = nullptr;
+    float eps = 0.f;
+    float *X = nullptr;
+    ActPtr Xa;
+};
+
+struct AttnArgs {
+    const float *qkv = nullptr;        // [Mpad][3E]: Q | K | V
+    const int32_t *offsets = nullptr;
+    int E = 0, H = 0;
+    float scale = 0.f;                 // 1.0f / sqrtf(d_head)
+    const uint16_t *exp_tab = nullptr; // fp16 -> fp16 exp table
+    ActPtr ctx;                        // [Mpad][E] activation format
+};
+
+constexpr int GEMM_BM = 64;   // rows per GEMM workgroup
+constexpr int ATT_QB = 64;    // queries per attention workgroup
+
+// Launchers (kernels.hip).  Return hipSuccess or the launch error.
+hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s);
+hipError_t launch_gemm(int wtype, int epi, int E_or_bn, const GemmArgs &a, int Mpad, hipStream_t s);
+hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs, int max_len, hipStream_t s);
+hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s);
+bool gemm_shape_supported(int epi, int N, int K);
+
+}  // namespace bertamd

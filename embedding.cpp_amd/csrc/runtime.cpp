@@ -1,0 +1,1009 @@
+// runtime.cpp — host runtime behind the reference C ABI (include/bert.h).
+//
+// Replaces the reference's bert.cpp runtime (loader bert.cpp:143-659, context
+// and arena bert.cpp:79-137/803-842, eval loop bert.cpp:1020-1108, encode
+// drivers bert.cpp:1110-1198) with:
+//   - a native GGUF reader (gguf_io.cpp) and the same hparam / tensor-shape
+//     validation as the reference loader (bert.cpp:496-513, 623-652);
+//   - per-device weight replicas, repacked once at load into MFMA fragment
+//     order (no per-call graph, no arena, no mem-per-token probe);
+//   - a fixed kernel pipeline over a ragged batch of sentences (kernels.hip);
+//   - data-parallel sharding of a batch over the context's devices, one host
+//     thread per device, no collectives.
+// Nothing throws across the ABI: load returns NULL, eval logs and returns.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bert.h"
+#include "bert_amd.h"
+#include "ggml_formats.h"
+#include "gguf_io.h"
+#include "kernels.h"
+#include "tokenizer.h"
+
+using namespace bertamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+#define HIP_OK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            set_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return false;                                                             \
+        }                                                                             \
+    } while (0)
+
+// ggml_init's fp16 tables (GELU tanh form and exp), built with this host's libm
+// exactly like ggml builds them.
+struct HostTables {
+    std::vector<uint16_t> gelu, expt;
+    HostTables() : gelu(65536), expt(65536) {
+        const float A = 0.044715f, S = 0.79788456080286535587989211986876f;
+        for (int i = 0; i < 65536; i++) {
+            const float f = f16_to_f32((uint16_t)i);
+            const float g = 0.5f * f * (1.0f + tanhf(S * f * fmaf(A * f, f, 1.0f)));
+            gelu[i] = f32_to_f16(g);
+            expt[i] = f32_to_f16(expf(f));
+        }
+    }
+};
+const HostTables &tables() {
+    static HostTables t;
+    return t;
+}
+
+struct HParams {
+    int32_t n_vocab = 0, n_max_tokens = 0, n_embd = 0, n_intermediate = 0, n_head = 0, n_layer = 0;
+    float eps = 1e-12f;
+};
+
+struct DevMat {
+    WPtr w;
+};
+
+struct DevLayer {
+    WPtr qkv, o, up, down;
+    float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
+    float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
+};
+
+struct Workspace {
+    int64_t cap_rows = 0;   // padded rows
+    int64_t cap_seqs = 0;
+    float *X = nullptr, *QKV = nullptr, *out = nullptr;
+    ActPtr Xa, Ca, Ua;
+    int32_t *tok = nullptr, *off = nullptr;
+    std::vector<void *> allocs;
+    // pinned host staging for the host-pointer ABI
+    int32_t *h_tok = nullptr, *h_off = nullptr;
+    float *h_out = nullptr;
+    int64_t h_cap_rows = 0, h_cap_seqs = 0;
+};
+
+struct ProfEntry {
+    double ms = 0;
+    int64_t n = 0;
+};
+
+struct Replica {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void *word = nullptr, *pos = nullptr, *type = nullptr;
+    float *ln_e_w = nullptr, *ln_e_b = nullptr;
+    std::vector<DevLayer> L;
+    uint16_t *gelu_tab = nullptr, *exp_tab = nullptr;
+    std::vector<void *> weight_allocs;
+    Workspace ws;
+    // profiling: events recorded around each launch when enabled
+    bool prof = false;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::map<std::string, ProfEntry> prof_acc;
+};
+
+int wtype_of(uint32_t ggml_type) {
+    switch (ggml_type) {
+        case GT_F32: return W_F32;
+        case GT_F16: return W_F16;
+        case GT_Q4_0: return W_Q4_0;
+        case GT_Q4_1: return W_Q4_1;
+    }
+    return -1;
+}
+
+}  // namespace
+
+struct bert_ctx {
+    HParams hp;
+    int wtype = 0;                      // kernels.h WType of the 2-D weights
+    uint32_t word_t = 0, pos_t = 0, type_t = 0;
+    std::vector<std::string> id_to_token;
+    int32_t cls_id = 101, sep_id = 102, pad_id = 0;
+    WordPieceTokenizer tokenizer;
+    std::vector<std::unique_ptr<Replica>> reps;
+    std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
+};
+
+namespace {
+
+template <typename T>
+bool dmalloc(std::vector<void *> &track, T **p, size_t bytes) {
+    void *q = nullptr;
+    HIP_OK(hipMalloc(&q, bytes < 16 ? 16 : bytes));
+    track.push_back(q);
+    *p = (T *)q;
+    return true;
+}
+
+template <typename T>
+bool upload(std::vector<void *> &track, T **p, const void *src, size_t bytes) {
+    if (!dmalloc(track, p, bytes)) return false;
+    HIP_OK(hipMemcpy(*p, src, bytes, hipMemcpyHostToDevice));
+    return true;
+}
+
+// Repack a [N][K] ggml-format matrix (given as row pointers) into MFMA
+// fragment order (kernels.h WPtr).
+struct Packed {
+    std::vector<uint8_t> q, d, m;
+};
+
+Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows, int64_t K) {
+    const int64_t N = (int64_t)rows.size(), nkb = K / 32, ntl = N / 16;
+    Packed p;
+    if (type == GT_Q4_0 || type == GT_Q4_1) {
+        const int bs = type == GT_Q4_0 ? 18 : 20, qoff = type == GT_Q4_0 ? 2 : 4;
+        p.q.resize((size_t)ntl * nkb * 64 * 4);
+        p.d.resize((size_t)ntl * nkb * 16 * 2);
+        if (type == GT_Q4_1) p.m.resize(p.d.size());
+        uint32_t *q = (uint32_t *)p.q.data();
+        uint16_t *d = (uint16_t *)p.d.data(), *m = (uint16_t *)p.m.data();
+        for (int64_t nt = 0; nt < ntl; nt++)
+            for (int64_t kb = 0; kb < nkb; kb++) {
+                const int64_t t = nt * nkb + kb;
+                for (int lane = 0; lane < 64; lane++) {
+                    const int c = lane & 15, g = lane >> 4;
+                    const uint8_t *blk = rows[nt * 16 + c] + kb * bs;
+                    uint32_t x = 0;
+                    for (int s = 0; s < 8; s++) {
+                        const int e = 8 * g + (s < 4 ? 2 * s : 2 * (s - 4) + 1);
+                        const uint8_t byte = blk[qoff + (e & 15)];
+                        const uint32_t qv = e < 16 ? (byte & 15u) : (byte >> 4);
+                        x |= qv << (4 * s);
+                    }
+                    q[t * 64 + lane] = x;
+                    if (g == 0) {
+                        std::memcpy(&d[t * 16 + c], blk, 2);
+                        if (type == GT_Q4_1) std::memcpy(&m[t * 16 + c], blk + 2, 2);
+                    }
+                }
+            }
+    } else if (type == GT_F16) {
+        p.q.resize((size_t)N * K * 2);
+        uint16_t *q = (uint16_t *)p.q.data();
+        for (int64_t nt = 0; nt < ntl; nt++)
+            for (int64_t kb = 0; kb < nkb; kb++)
+                for (int lane = 0; lane < 64; lane++) {
+                    const int c = lane & 15, g = lane >> 4;
+                    const uint16_t *src = (const uint16_t *)rows[nt * 16 + c] + kb * 32 + 8 * g;
+                    std::memcpy(&q[((nt * nkb + kb) * 64 + lane) * 8], src, 16);
+                }
+    } else {
+        p.q.resize((size_t)N * K * 4);
+        float *q = (float *)p.q.data();
+        for (int64_t nt = 0; nt < ntl; nt++)
+            for (int64_t kb = 0; kb < nkb; kb++)
+                for (int lane = 0; lane < 64; lane++) {
+                    const int c = lane & 15, g = lane >> 4;
+                    const float *src = (const float *)rows[nt * 16 + c] + kb * 32;
+                    float *dst = &q[((nt * nkb + kb) * 64 + lane) * 8];
+                    for (int cc = 0; cc < 2; cc++)
+                        for (int j = 0; j < 4; j++) dst[cc * 4 + j] = src[16 * cc + 4 * g + j];
+                }
+    }
+    return p;
+}
+
+bool upload_packed(std::vector<void *> &track, WPtr &w, const Packed &p) {
+    void *q = nullptr, *d = nullptr, *m = nullptr;
+    if (!upload(track, &q, p.q.data(), p.q.size())) return false;
+    if (!p.d.empty() && !upload(track, &d, p.d.data(), p.d.size())) return false;
+    if (!p.m.empty() && !upload(track, &m, p.m.data(), p.m.size())) return false;
+    w.q = q;
+    w.d = d;
+    w.m = m;
+    return true;
+}
+
+std::vector<const uint8_t *> rows_of(const GGUFTensor *t) {
+    const size_t rb = ggml_row_bytes(t->type, t->ne[0]);
+    std::vector<const uint8_t *> r((size_t)t->ne[1]);
+    for (int64_t i = 0; i < t->ne[1]; i++) r[(size_t)i] = t->data + (size_t)i * rb;
+    return r;
+}
+
+size_t act_elem_bytes(int wtype) { return wtype == W_F32 ? 4 : wtype == W_F16 ? 2 : 1; }
+size_t act_scale_bytes(int wtype) { return wtype == W_Q4_0 ? 2 : wtype == W_Q4_1 ? 4 : 0; }
+
+bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, int64_t K) {
+    if (!dmalloc(track, &a.q, (size_t)rows * K * act_elem_bytes(wtype))) return false;
+    if (act_scale_bytes(wtype) && !dmalloc(track, &a.d, (size_t)rows * (K / 32) * act_scale_bytes(wtype)))
+        return false;
+    return true;
+}
+
+bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs) {
+    Workspace &w = R.ws;
+    if (Mpad <= w.cap_rows && n_seqs <= w.cap_seqs) return true;
+    HIP_OK(hipStreamSynchronize(R.stream));
+    for (void *p : w.allocs) hipFree(p);
+    w.allocs.clear();
+    const int64_t rows = std::max<int64_t>(Mpad, w.cap_rows), seqs = std::max<int64_t>(n_seqs, w.cap_seqs);
+    const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
+    const int wt = ctx->wtype;
+    if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.QKV, (size_t)rows * 3 * E * 4) ||
+        !alloc_act(w.allocs, w.Xa, wt, rows, E) || !alloc_act(w.allocs, w.Ca, wt, rows, E) ||
+        !alloc_act(w.allocs, w.Ua, wt, rows, I) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
+        !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4))
+        return false;
+    // padding rows must hold finite values: zero everything once
+    HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, R.stream));
+    HIP_OK(hipMemsetAsync(w.QKV, 0, (size_t)rows * 3 * E * 4, R.stream));
+    w.cap_rows = rows;
+    w.cap_seqs = seqs;
+    return true;
+}
+
+// ---- profiling helpers
+struct Launch {
+    Replica &R;
+    hipStream_t s;
+    const char *name;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    Launch(Replica &r, hipStream_t st, const char *n) : R(r), s(st), name(n) {
+        if (R.prof) {
+            hipEventCreate(&e0);
+            hipEventCreate(&e1);
+            hipEventRecord(e0, s);
+        }
+    }
+    ~Launch() {
+        if (R.prof) {
+            hipEventRecord(e1, s);
+            R.pending.push_back({name, {e0, e1}});
+        }
+    }
+};
+
+void drain_profile(Replica &R) {
+    for (auto &p : R.pending) {
+        hipEventSynchronize(p.second.second);
+        float ms = 0;
+        hipEventElapsedTime(&ms, p.second.first, p.second.second);
+        auto &e = R.prof_acc[p.first];
+        e.ms += ms;
+        e.n += 1;
+        hipEventDestroy(p.second.first);
+        hipEventDestroy(p.second.second);
+    }
+    R.pending.clear();
+}
+
+#define LAUNCH_OK(name, expr)                                                             \
+    do {                                                                                  \
+        Launch lp_(R, st, name);                                                          \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            set_err("kernel %s launch failed: %s", name, hipGetErrorString(e_));          \
+            return false;                                                                 \
+        }                                                                                 \
+    } while (0)
+
+// The fixed pipeline over a ragged batch already resident on the device.
+bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
+                  int n_seqs, float *d_out, hipStream_t st) {
+    const HParams &hp = ctx->hp;
+    const int64_t M = h_off[n_seqs];
+    const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
+    int max_len = 0;
+    for (int s = 0; s < n_seqs; s++) max_len = std::max(max_len, h_off[s + 1] - h_off[s]);
+    if (!ensure_workspace(ctx, R, Mpad, n_seqs)) return false;
+    Workspace &w = R.ws;
+    const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
+
+    EmbedArgs ea;
+    ea.tokens = d_tok;
+    ea.offsets = d_off;
+    ea.n_seqs = n_seqs;
+    ea.M = (int)M;
+    ea.E = E;
+    ea.n_vocab = hp.n_vocab;
+    ea.n_pos = hp.n_max_tokens;
+    ea.word = R.word;
+    ea.pos = R.pos;
+    ea.type = R.type;
+    ea.word_t = wtype_of(ctx->word_t);
+    ea.pos_t = wtype_of(ctx->pos_t);
+    ea.type_t = wtype_of(ctx->type_t);
+    ea.ln_w = R.ln_e_w;
+    ea.ln_b = R.ln_e_b;
+    ea.eps = hp.eps;
+    ea.X = w.X;
+    ea.Xa = w.Xa;
+    LAUNCH_OK("embed_ln", launch_embed(wt, ea, (int)Mpad, st));
+
+    for (int il = 0; il < hp.n_layer; il++) {
+        const DevLayer &L = R.L[il];
+        GemmArgs q;
+        q.A = w.Xa;
+        q.K = E;
+        q.W = L.qkv;
+        q.N = 3 * E;
+        q.bias = L.b_qkv;
+        q.out_f32 = w.QKV;
+        LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_BIAS_F32, 0, q, (int)Mpad, st));
+
+        AttnArgs aa;
+        aa.qkv = w.QKV;
+        aa.offsets = d_off;
+        aa.E = E;
+        aa.H = H;
+        aa.scale = 1.0f / sqrtf((float)D);
+        aa.exp_tab = R.exp_tab;
+        aa.ctx = w.Ca;
+        LAUNCH_OK("attention", launch_attention(wt, D, aa, n_seqs, max_len, st));
+
+        GemmArgs o;
+        o.A = w.Ca;
+        o.K = E;
+        o.W = L.o;
+        o.N = E;
+        o.bias = L.b_o;
+        o.X = w.X;
+        o.out_act = w.Xa;
+        o.ln_w = L.ln1_w;
+        o.ln_b = L.ln1_b;
+        o.eps = hp.eps;
+        LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)Mpad, st));
+
+        GemmArgs u;
+        u.A = w.Xa;
+        u.K = E;
+        u.W = L.up;
+        u.N = I;
+        u.bias = L.b_up;
+        u.out_act = w.Ua;
+        u.gelu_tab = R.gelu_tab;
+        LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)Mpad, st));
+
+        GemmArgs dn;
+        dn.A = w.Ua;
+        dn.K = I;
+        dn.W = L.down;
+        dn.N = E;
+        dn.bias = L.b_down;
+        dn.X = w.X;
+        dn.out_act = w.Xa;
+        dn.ln_w = L.ln2_w;
+        dn.ln_b = L.ln2_b;
+        dn.eps = hp.eps;
+        LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)Mpad, st));
+    }
+    LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st));
+    return true;
+}
+
+// ---- loading
+const GGUFTensor *need_tensor(const GGUFFile &f, const std::string &name, std::vector<int64_t> ne) {
+    const GGUFTensor *t = f.tensor(name);
+    if (!t) {
+        set_err("tensor '%s' not found", name.c_str());
+        return nullptr;
+    }
+    for (size_t i = 0; i < ne.size(); i++)
+        if (i >= t->ne.size() || t->ne[i] != ne[i]) {
+            set_err("tensor '%s' has wrong shape", name.c_str());
+            return nullptr;
+        }
+    return t;
+}
+
+bool get_u32(const GGUFFile &f, const char *k, int32_t &out, bool req) {
+    const GGUFValue *v = f.find(k);
+    if (!v) {
+        if (req) set_err("key not found in model: %s", k);
+        return !req;
+    }
+    if (v->type != GV_U32) {
+        set_err("key %s has wrong type", k);
+        return false;
+    }
+    out = (int32_t)v->u;
+    return true;
+}
+
+struct HostModel {
+    const GGUFTensor *word, *pos, *type, *ln_e_w, *ln_e_b;
+    struct L {
+        const GGUFTensor *q_w, *q_b, *k_w, *k_b, *v_w, *v_b, *o_w, *o_b, *ln1_w, *ln1_b, *i_w, *i_b, *o2_w, *o2_b,
+            *ln2_w, *ln2_b;
+    };
+    std::vector<L> layers;
+};
+
+bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
+    R.device = device;
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
+    auto &tr = R.weight_allocs;
+    if (!upload(tr, &R.word, hm.word->data, hm.word->nbytes) || !upload(tr, &R.pos, hm.pos->data, hm.pos->nbytes) ||
+        !upload(tr, &R.type, hm.type->data, hm.type->nbytes) ||
+        !upload(tr, &R.ln_e_w, hm.ln_e_w->data, hm.ln_e_w->nbytes) ||
+        !upload(tr, &R.ln_e_b, hm.ln_e_b->data, hm.ln_e_b->nbytes) ||
+        !upload(tr, &R.gelu_tab, tables().gelu.data(), 65536 * 2) ||
+        !upload(tr, &R.exp_tab, tables().expt.data(), 65536 * 2))
+        return false;
+    const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
+    const uint32_t wt = hm.layers[0].q_w->type;
+    for (const auto &l : hm.layers) {
+        DevLayer dl;
+        std::vector<const uint8_t *> rows = rows_of(l.q_w), rk = rows_of(l.k_w), rv = rows_of(l.v_w);
+        rows.insert(rows.end(), rk.begin(), rk.end());
+        rows.insert(rows.end(), rv.begin(), rv.end());
+        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E)) || !upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E)) ||
+            !upload_packed(tr, dl.up, repack(wt, rows_of(l.i_w), E)) ||
+            !upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I)))
+            return false;
+        std::vector<float> bqkv((size_t)3 * E);
+        std::memcpy(bqkv.data(), l.q_b->data, E * 4);
+        std::memcpy(bqkv.data() + E, l.k_b->data, E * 4);
+        std::memcpy(bqkv.data() + 2 * E, l.v_b->data, E * 4);
+        if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
+            !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||
+            !upload(tr, &dl.ln1_w, l.ln1_w->data, E * 4) || !upload(tr, &dl.ln1_b, l.ln1_b->data, E * 4) ||
+            !upload(tr, &dl.ln2_w, l.ln2_w->data, E * 4) || !upload(tr, &dl.ln2_b, l.ln2_b->data, E * 4))
+            return false;
+        R.L.push_back(dl);
+    }
+    HIP_OK(hipDeviceSynchronize());
+    return true;
+}
+
+void free_replica(Replica &R) {
+    if (R.stream) {
+        hipSetDevice(R.device);
+        hipStreamSynchronize(R.stream);
+    }
+    drain_profile(R);
+    for (void *p : R.ws.allocs) hipFree(p);
+    for (void *p : R.weight_allocs) hipFree(p);
+    if (R.ws.h_tok) hipHostFree(R.ws.h_tok);
+    if (R.ws.h_off) hipHostFree(R.ws.h_off);
+    if (R.ws.h_out) hipHostFree(R.ws.h_out);
+    if (R.stream) hipStreamDestroy(R.stream);
+}
+
+std::vector<int> parse_device_env(int n_visible) {
+    std::vector<int> devs;
+    const char *env = std::getenv("BERT_AMD_DEVICES");
+    if (env && *env) {
+        std::string s(env);
+        size_t p = 0;
+        while (p < s.size()) {
+            size_t q = s.find(',', p);
+            if (q == std::string::npos) q = s.size();
+            int d = std::atoi(s.substr(p, q - p).c_str());
+            if (d >= 0 && d < n_visible) devs.push_back(d);
+            p = q + 1;
+        }
+    }
+    if (devs.empty())
+        for (int d = 0; d < n_visible; d++) devs.push_back(d);
+    return devs;
+}
+
+bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices) {
+    if (!fname) {
+        set_err("null model path");
+        return nullptr;
+    }
+    std::printf("%s: loading model from '%s' - please wait ...\n", "bert_load_from_file", fname);
+    GGUFFile f;
+    std::string err;
+    if (!f.open(fname, err)) {
+        set_err("%s", err.c_str());
+        return nullptr;
+    }
+    auto ctx = std::make_unique<bert_ctx>();
+    HParams &hp = ctx->hp;
+    // reference bert.cpp:506-512
+    const GGUFValue *toks = f.find("tokenizer.ggml.tokens");
+    if (!toks || toks->type != GV_ARR || toks->arr_type != GV_STR) {
+        set_err("cannot find tokenizer vocab in model file");
+        return nullptr;
+    }
+    hp.n_vocab = (int32_t)toks->arr_n;
+    if (!get_u32(f, "bert.context_length", hp.n_max_tokens, true) ||
+        !get_u32(f, "bert.embedding_length", hp.n_embd, true) ||
+        !get_u32(f, "bert.feed_forward_length", hp.n_intermediate, true) ||
+        !get_u32(f, "bert.attention.head_count", hp.n_head, true) ||
+        !get_u32(f, "bert.block_count", hp.n_layer, true))
+        return nullptr;
+    const GGUFValue *eps = f.find("bert.attention.layer_norm_epsilon");
+    if (!eps || eps->type != GV_F32) {
+        set_err("key not found in model: bert.attention.layer_norm_epsilon");
+        return nullptr;
+    }
+    hp.eps = (float)eps->f;
+    // tokenizer (reference bert.cpp:515-578)
+    if (!f.find("tokenizer.ggml.scores")) { set_err("cannot find tokenizer scores in model file"); return nullptr; }
+    if (!f.find("tokenizer.ggml.token_type")) { set_err("cannot find token type list in GGUF file"); return nullptr; }
+    ctx->id_to_token = toks->arr_str;
+    get_u32(f, "tokenizer.ggml.cls_token_id", ctx->cls_id, false);
+    get_u32(f, "tokenizer.ggml.seperator_token_id", ctx->sep_id, false);
+    get_u32(f, "tokenizer.ggml.padding_token_id", ctx->pad_id, false);
+    const GGUFValue *blob = f.find("blob.tokenizer.json");
+    if (!blob || blob->type != GV_STR) {
+        set_err("key not found in model: blob.tokenizer.json");
+        return nullptr;
+    }
+    if (!ctx->tokenizer.load(blob->s, err)) {
+        set_err("%s", err.c_str());
+        return nullptr;
+    }
+    // tensors (reference bert.cpp:623-652)
+    const int64_t E = hp.n_embd, I = hp.n_intermediate;
+    HostModel hm;
+    if (!(hm.word = need_tensor(f, "embeddings.word_embeddings.weight", {E, hp.n_vocab})) ||
+        !(hm.type = need_tensor(f, "embeddings.token_type_embeddings.weight", {E, 2})) ||
+        !(hm.pos = need_tensor(f, "embeddings.position_embeddings.weight", {E, hp.n_max_tokens})) ||
+        !(hm.ln_e_w = need_tensor(f, "embeddings.LayerNorm.weight", {E})) ||
+        !(hm.ln_e_b = need_tensor(f, "embeddings.LayerNorm.bias", {E})))
+        return nullptr;
+    for (int il = 0; il < hp.n_layer; il++) {
+        const std::string p = "encoder.layer." + std::to_string(il) + ".";
+        HostModel::L l;
+        if (!(l.ln1_w = need_tensor(f, p + "attention.output.LayerNorm.weight", {E})) ||
+            !(l.ln1_b = need_tensor(f, p + "attention.output.LayerNorm.bias", {E})) ||
+            !(l.ln2_w = need_tensor(f, p + "output.LayerNorm.weight", {E})) ||
+            !(l.ln2_b = need_tensor(f, p + "output.LayerNorm.bias", {E})) ||
+            !(l.q_w = need_tensor(f, p + "attention.self.query.weight", {E, E})) ||
+            !(l.q_b = need_tensor(f, p + "attention.self.query.bias", {E})) ||
+            !(l.k_w = need_tensor(f, p + "attention.self.key.weight", {E, E})) ||
+            !(l.k_b = need_tensor(f, p + "attention.self.key.bias", {E})) ||
+            !(l.v_w = need_tensor(f, p + "attention.self.value.weight", {E, E})) ||
+            !(l.v_b = need_tensor(f, p + "attention.self.value.bias", {E})) ||
+            !(l.o_w = need_tensor(f, p + "attention.output.dense.weight", {E, E})) ||
+            !(l.o_b = need_tensor(f, p + "attention.output.dense.bias", {E})) ||
+            !(l.i_w = need_tensor(f, p + "intermediate.dense.weight", {E, I})) ||
+            !(l.i_b = need_tensor(f, p + "intermediate.dense.bias", {I})) ||
+            !(l.o2_w = need_tensor(f, p + "output.dense.weight", {I, E})) ||
+            !(l.o2_b = need_tensor(f, p + "output.dense.bias", {E})))
+            return nullptr;
+        hm.layers.push_back(l);
+    }
+    // one weight type for the 2-D matrices; 1-D tensors must be f32
+    const uint32_t wt = hm.layers[0].q_w->type;
+    ctx->wtype = wtype_of(wt);
+    if (ctx->wtype < 0) { set_err("unsupported weight type %u", wt); return nullptr; }
+    for (auto &l : hm.layers) {
+        for (const GGUFTensor *t : {l.q_w, l.k_w, l.v_w, l.o_w, l.i_w, l.o2_w})
+            if (t->type != wt) { set_err("mixed weight types are not supported (%s)", t->name.c_str()); return nullptr; }
+        for (const GGUFTensor *t : {l.q_b, l.k_b, l.v_b, l.o_b, l.i_b, l.o2_b, l.ln1_w, l.ln1_b, l.ln2_w, l.ln2_b})
+            if (t->type != GT_F32) { set_err("1-D tensor %s is not f32", t->name.c_str()); return nullptr; }
+    }
+    for (const GGUFTensor *t : {hm.word, hm.pos, hm.type})
+        if (wtype_of(t->type) < 0) { set_err("unsupported embedding table type for %s", t->name.c_str()); return nullptr; }
+    if (hm.ln_e_w->type != GT_F32 || hm.ln_e_b->type != GT_F32) { set_err("embedding LayerNorm must be f32"); return nullptr; }
+    ctx->word_t = hm.word->type;
+    ctx->pos_t = hm.pos->type;
+    ctx->type_t = hm.type->type;
+    const int D = (int)(E / hp.n_head);
+    if ((E != 384 && E != 768 && E != 1024) || (D != 32 && D != 64) || I % 256 || hp.n_max_tokens > 512 ||
+        !gemm_shape_supported(EPI_BIAS_F32, (int)(3 * E), (int)E) || !gemm_shape_supported(EPI_LN, (int)E, (int)I)) {
+        set_err("unsupported shape: n_embd=%d n_head=%d n_intermediate=%d n_max_tokens=%d", hp.n_embd, hp.n_head,
+                hp.n_intermediate, hp.n_max_tokens);
+        return nullptr;
+    }
+    // devices
+    int n_visible = 0;
+    if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {
+        set_err("no HIP device visible: this library runs the embedding path on MI355X GPUs only");
+        return nullptr;
+    }
+    std::vector<int> devs;
+    if (devices && n_devices > 0) {
+        for (int i = 0; i < n_devices; i++)
+            if (devices[i] >= 0 && devices[i] < n_visible) devs.push_back(devices[i]);
+    } else {
+        devs = parse_device_env(n_visible);
+    }
+    if (devs.empty()) { set_err("no usable device in the requested list"); return nullptr; }
+    for (int d : devs) {
+        auto R = std::make_unique<Replica>();
+        if (!build_replica(ctx.get(), hm, d, *R)) {
+            free_replica(*R);
+            for (auto &r : ctx->reps) free_replica(*r);
+            return nullptr;
+        }
+        ctx->reps.push_back(std::move(R));
+    }
+    std::printf("%s: n_vocab = %d, n_max_tokens = %d, n_embd = %d, n_intermediate = %d, n_head = %d, n_layer = %d, "
+                "weights = %s, devices = %zu\n",
+                "bert_load_from_file", hp.n_vocab, hp.n_max_tokens, hp.n_embd, hp.n_intermediate, hp.n_head,
+                hp.n_layer, ggml_type_str(wt), devs.size());
+    return ctx.release();
+}
+
+bool grow_pinned(Workspace &w, int64_t rows, int64_t seqs, int64_t E) {
+    if (rows > w.h_cap_rows) {
+        if (w.h_tok) hipHostFree(w.h_tok);
+        w.h_tok = nullptr;
+        HIP_OK(hipHostMalloc((void **)&w.h_tok, (size_t)rows * 4, hipHostMallocDefault));
+        w.h_cap_rows = rows;
+    }
+    if (seqs > w.h_cap_seqs) {
+        if (w.h_off) hipHostFree(w.h_off);
+        if (w.h_out) hipHostFree(w.h_out);
+        w.h_off = nullptr;
+        w.h_out = nullptr;
+        HIP_OK(hipHostMalloc((void **)&w.h_off, (size_t)(seqs + 1) * 4, hipHostMallocDefault));
+        HIP_OK(hipHostMalloc((void **)&w.h_out, (size_t)seqs * E * 4, hipHostMallocDefault));
+        w.h_cap_seqs = seqs;
+    }
+    return true;
+}
+
+// Evaluate sentences [s0, s1) of a host batch on replica R; results go
+// straight into the caller's embedding rows.
+bool eval_host_slice(bert_ctx *ctx, Replica &R, bert_vocab_id **toks, const int32_t *ntok, float **embs, int s0,
+                     int s1) {
+    const int n = s1 - s0;
+    if (n <= 0) return true;
+    HIP_OK(hipSetDevice(R.device));
+    int64_t M = 0;
+    for (int s = s0; s < s1; s++) M += ntok[s];
+    if (!grow_pinned(R.ws, M, n, ctx->hp.n_embd)) return false;
+    Workspace &w = R.ws;
+    int64_t pos = 0;
+    for (int s = s0; s < s1; s++) {
+        w.h_off[s - s0] = (int32_t)pos;
+        std::memcpy(w.h_tok + pos, toks[s], (size_t)ntok[s] * 4);
+        pos += ntok[s];
+    }
+    w.h_off[n] = (int32_t)pos;
+    const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
+    if (!ensure_workspace(ctx, R, Mpad, n)) return false;
+    const hipStream_t st = R.stream;
+    HIP_OK(hipMemcpyAsync(w.tok, w.h_tok, (size_t)M * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(w.off, w.h_off, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
+    if (!run_pipeline(ctx, R, w.tok, w.off, w.h_off, n, w.out, st)) return false;
+    const int E = ctx->hp.n_embd;
+    HIP_OK(hipMemcpyAsync(w.h_out, w.out, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    drain_profile(R);
+    for (int s = s0; s < s1; s++) std::memcpy(embs[s], w.h_out + (size_t)(s - s0) * E, (size_t)E * 4);
+    return true;
+}
+
+// Host-pointer batch eval, sharded over the context's replicas by token count.
+void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
+    if (!ctx || n <= 0 || !toks || !ntok || !embs) return;
+    for (int s = 0; s < n; s++) {
+        if (ntok[s] > ctx->hp.n_max_tokens) {
+            std::fprintf(stderr, "Too many tokens, maximum is %d\n", ctx->hp.n_max_tokens);
+            return;
+        }
+        if (ntok[s] <= 0 || !toks[s] || !embs[s]) {
+            std::fprintf(stderr, "%s: empty input %d\n", __func__, s);
+            return;
+        }
+        for (int t = 0; t < ntok[s]; t++)
+            if (toks[s][t] < 0 || toks[s][t] >= ctx->hp.n_vocab) {
+                std::fprintf(stderr, "%s: token id %d out of range\n", __func__, toks[s][t]);
+                return;
+            }
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const int nr = (int)ctx->reps.size();
+    // contiguous slices balanced by token count
+    std::vector<int> cut(nr + 1, n);
+    cut[0] = 0;
+    int64_t total = 0;
+    for (int s = 0; s < n; s++) total += ntok[s];
+    {
+        int64_t acc = 0;
+        int r = 1;
+        for (int s = 0; s < n && r < nr; s++) {
+            acc += ntok[s];
+            while (r < nr && acc * nr >= total * r) cut[r++] = s + 1;
+        }
+        for (; r < nr; r++) cut[r] = n;
+    }
+    if (nr == 1) {
+        if (!eval_host_slice(ctx, *ctx->reps[0], toks, ntok, embs, 0, n))
+            std::fprintf(stderr, "bert_eval_batch: %s\n", g_err.c_str());
+        return;
+    }
+    std::vector<std::thread> th;
+    std::vector<std::string> errs(nr);
+    for (int r = 0; r < nr; r++)
+        th.emplace_back([&, r] {
+            if (!eval_host_slice(ctx, *ctx->reps[r], toks, ntok, embs, cut[r], cut[r + 1])) errs[r] = g_err;
+        });
+    for (auto &t : th) t.join();
+    for (int r = 0; r < nr; r++)
+        if (!errs[r].empty()) std::fprintf(stderr, "bert_eval_batch: device %d: %s\n", ctx->reps[r]->device, errs[r].c_str());
+}
+
+}  // namespace
+
+// ============================================================ C ABI (bert.h)
+
+bool bert_params_parse(int argc, char **argv, bert_params &params) {
+    // reference bert.cpp:681-733 (same flags; -s is advertised there but rejected too)
+    auto usage = [&](FILE *o) {
+        std::fprintf(o, "usage: %s [options]\n\noptions:\n", argv[0]);
+        std::fprintf(o, "  -h, --help            show this help message and exit\n");
+        std::fprintf(o, "  -t N, --threads N     number of threads to use during computation (default: %d)\n", params.n_threads);
+        std::fprintf(o, "  -p PROMPT, --prompt PROMPT\n                        prompt to start generation with (default: random)\n");
+        std::fprintf(o, "  --port p     port to bind in server mode (default: %d)\n", params.port);
+        std::fprintf(o, "  -m FNAME, --model FNAME\n                        model path (default: %s)\n\n", params.model);
+    };
+    for (int i = 1; i < argc; i++) {
+        const std::string arg = argv[i];
+        const bool has_val = i + 1 < argc;
+        if ((arg == "-t" || arg == "--threads") && has_val) params.n_threads = std::atoi(argv[++i]);
+        else if ((arg == "-p" || arg == "--prompt") && has_val) params.prompt = argv[++i];
+        else if (arg == "--port" && has_val) params.port = std::atoi(argv[++i]);
+        else if ((arg == "-m" || arg == "--model") && has_val) params.model = argv[++i];
+        else if (arg == "-h" || arg == "--help") { usage(stderr); std::exit(0); }
+        else {
+            std::fprintf(stderr, "error: unknown argument: %s\n", arg.c_str());
+            usage(stderr);
+            std::exit(0);
+        }
+    }
+    return true;
+}
+
+bert_ctx *bert_load_from_file(const char *fname) {
+    bert_ctx *c = nullptr;
+    try {
+        c = load_impl(fname, nullptr, 0);
+    } catch (const std::exception &e) {
+        set_err("%s", e.what());
+        c = nullptr;
+    }
+    if (!c) std::fprintf(stderr, "bert_load_from_file: %s\n", g_err.c_str());
+    return c;
+}
+
+void bert_free(bert_ctx *ctx) {
+    if (!ctx) return;
+    for (auto &r : ctx->reps) free_replica(*r);
+    delete ctx;
+}
+
+namespace {
+// reference bert.cpp:738-781: [CLS] + Encode(text) up to the first pad id +
+// [SEP], truncated so that the last slot is [SEP].
+int32_t frame_tokens(const std::vector<int32_t> &ids, int32_t cls, int32_t sep, int32_t pad, bert_vocab_id *tokens,
+                     int32_t n_max_tokens) {
+    int32_t t = 0;
+    tokens[t++] = cls;
+    for (int32_t id : ids) {
+        if (id == pad) break;
+        if (t >= n_max_tokens) break;
+        tokens[t++] = id;
+        if (t >= n_max_tokens) break;
+    }
+    if (t >= n_max_tokens) tokens[n_max_tokens - 1] = sep;
+    else tokens[t++] = sep;
+    return t;
+}
+}  // namespace
+
+void bert_tokenize(bert_ctx *ctx, const char *text, bert_vocab_id *tokens, int32_t *n_tokens, int32_t n_max_tokens) {
+    if (!ctx || !text || !tokens || !n_tokens || n_max_tokens <= 0) return;
+    std::vector<int32_t> ids;
+    try {
+        ids = ctx->tokenizer.encode(text);
+    } catch (...) {
+        ids.clear();
+    }
+    *n_tokens = frame_tokens(ids, ctx->cls_id, ctx->sep_id, ctx->pad_id, tokens, n_max_tokens);
+}
+
+void bert_eval(bert_ctx *ctx, int32_t n_threads, bert_vocab_id *tokens, int32_t n_tokens, float *embeddings) {
+    // reference bert.cpp:1020-1028; embeddings == NULL was the reference's
+    // arena-probe mode: nothing to probe here, so it is a no-op.
+    (void)n_threads;
+    if (!embeddings) return;
+    bert_eval_batch(ctx, n_threads, 1, &tokens, &n_tokens, &embeddings);
+}
+
+void bert_eval_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, bert_vocab_id **batch_tokens,
+                     int32_t *n_tokens, float **batch_embeddings) {
+    (void)n_threads;
+    if (!batch_embeddings) return;
+    try {
+        eval_batch_impl(ctx, n_batch_size, batch_tokens, n_tokens, batch_embeddings);
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "bert_eval_batch: %s\n", e.what());
+    }
+}
+
+void bert_encode(bert_ctx *ctx, int32_t n_threads, const char *texts, float *embeddings) {
+    bert_encode_batch(ctx, n_threads, 1, 1, &texts, &embeddings);
+}
+
+void bert_encode_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, int32_t n_inputs, const char **texts,
+                       float **embeddings) {
+    // reference bert.cpp:1119-1198 tokenises everything, sorts by length and
+    // evaluates one sentence at a time; here the whole set is one ragged
+    // batch (n_batch_size only bounds the per-call working set).
+    if (!ctx || n_inputs <= 0 || !texts || !embeddings) return;
+    const int32_t N = ctx->hp.n_max_tokens;
+    std::vector<bert_vocab_id> buf((size_t)N * n_inputs);
+    std::vector<int32_t> ntok(n_inputs);
+    std::vector<bert_vocab_id *> ptr(n_inputs);
+    bert_vocab_id *ids = buf.data();
+    for (int i = 0; i < n_inputs; i++) {
+        ptr[i] = ids;
+        bert_tokenize(ctx, texts[i], ids, &ntok[i], N);
+        ids += ntok[i];
+    }
+    const int32_t chunk = std::max<int32_t>(n_inputs, std::max<int32_t>(n_batch_size, 1));
+    for (int32_t i = 0; i < n_inputs; i += chunk) {
+        const int32_t m = std::min(chunk, n_inputs - i);
+        bert_eval_batch(ctx, n_threads, m, ptr.data() + i, ntok.data() + i, embeddings + i);
+    }
+}
+
+int32_t bert_n_embd(bert_ctx *ctx) { return ctx ? ctx->hp.n_embd : 0; }
+int32_t bert_n_max_tokens(bert_ctx *ctx) { return ctx ? ctx->hp.n_max_tokens : 0; }
+
+const char *bert_vocab_id_to_token(bert_ctx *ctx, bert_vocab_id id) {
+    if (!ctx || id < 0 || (size_t)id >= ctx->id_to_token.size()) return "";
+    return ctx->id_to_token[(size_t)id].c_str();
+}
+
+// ============================================================ extensions (bert_amd.h)
+
+bert_ctx *bert_amd_load(const char *fname, const int32_t *devices, int32_t n_devices) {
+    try {
+        return load_impl(fname, devices, n_devices);
+    } catch (const std::exception &e) {
+        set_err("%s", e.what());
+        return nullptr;
+    }
+}
+
+int32_t bert_amd_n_devices(bert_ctx *ctx) { return ctx ? (int32_t)ctx->reps.size() : 0; }
+
+int32_t bert_amd_hparams(bert_ctx *ctx, int32_t *o) {
+    if (!ctx || !o) return -1;
+    const HParams &h = ctx->hp;
+    o[0] = h.n_vocab; o[1] = h.n_max_tokens; o[2] = h.n_embd; o[3] = h.n_intermediate;
+    o[4] = h.n_head; o[5] = h.n_layer; o[6] = ctx->wtype;
+    return 0;
+}
+
+int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_tokens, const int32_t *d_offsets,
+                             const int32_t *h_offsets, int32_t n_seqs, float *d_out, void *hip_stream) {
+    if (!ctx || slot < 0 || slot >= (int32_t)ctx->reps.size() || !d_tokens || !d_offsets || !h_offsets || n_seqs <= 0 ||
+        !d_out) {
+        set_err("bert_amd_eval_device: invalid arguments");
+        return -1;
+    }
+    for (int s = 0; s < n_seqs; s++) {
+        const int32_t n = h_offsets[s + 1] - h_offsets[s];
+        if (n <= 0 || n > ctx->hp.n_max_tokens) {
+            set_err("bert_amd_eval_device: sentence %d has %d tokens (max %d)", s, n, ctx->hp.n_max_tokens);
+            return -2;
+        }
+    }
+    Replica &R = *ctx->reps[slot];
+    if (hipSetDevice(R.device) != hipSuccess) { set_err("hipSetDevice failed"); return -3; }
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : R.stream;
+    try {
+        if (!run_pipeline(ctx, R, d_tokens, d_offsets, h_offsets, n_seqs, d_out, st)) return -4;
+    } catch (const std::exception &e) {
+        set_err("%s", e.what());
+        return -5;
+    }
+    return 0;
+}
+
+int32_t bert_amd_profile_enable(bert_ctx *ctx, int32_t enable) {
+    if (!ctx) return -1;
+    for (auto &r : ctx->reps) {
+        hipSetDevice(r->device);
+        hipDeviceSynchronize();
+        drain_profile(*r);
+        r->prof = enable != 0;
+        r->prof_acc.clear();
+    }
+    return 0;
+}
+
+int32_t bert_amd_profile_read(bert_ctx *ctx, char *names_buf, int32_t names_len, float *total_ms, int32_t *counts,
+                              int32_t max_entries) {
+    if (!ctx) return -1;
+    std::map<std::string, ProfEntry> agg;
+    for (auto &r : ctx->reps) {
+        hipSetDevice(r->device);
+        hipDeviceSynchronize();
+        drain_profile(*r);
+        for (auto &kv : r->prof_acc) {
+            agg[kv.first].ms += kv.second.ms;
+            agg[kv.first].n += kv.second.n;
+        }
+    }
+    int i = 0, off = 0;
+    for (auto &kv : agg) {
+        if (i >= max_entries) break;
+        const int need = (int)kv.first.size() + 1;
+        if (names_buf && off + need <= names_len) {
+            std::memcpy(names_buf + off, kv.first.c_str(), need);
+            off += need;
+        }
+        if (total_ms) total_ms[i] = (float)kv.second.ms;
+        if (counts) counts[i] = (int32_t)kv.second.n;
+        i++;
+    }
+    return i;
+}
+
+const char *bert_amd_last_error(void) { return g_err.c_str(); }
+
+int32_t bert_amd_tokenize_json(const char *tokenizer_json, const char *text, int32_t *tokens, int32_t n_max_tokens,
+                               int32_t frame, int32_t cls_id, int32_t sep_id, int32_t pad_id) {
+    if (!tokenizer_json || !text || !tokens || n_max_tokens <= 0) {
+        set_err("bert_amd_tokenize_json: invalid arguments");
+        return -1;
+    }
+    try {
+        WordPieceTokenizer tk;
+        std::string err;
+        if (!tk.load(tokenizer_json, err)) {
+            set_err("%s", err.c_str());
+            return -2;
+        }
+        const std::vector<int32_t> ids = tk.encode(text);
+        if (frame) return frame_tokens(ids, cls_id, sep_id, pad_id, tokens, n_max_tokens);
+        const int32_t n = (int32_t)std::min<size_t>(ids.size(), (size_t)n_max_tokens);
+        std::copy(ids.begin(), ids.begin() + n, tokens);
+        return n;
+    } catch (const std::exception &e) {
+        set_err("%s", e.what());
+        return -3;
+    }
+}

@@ -1,0 +1,44 @@
+// tokenizer.h — native BERT WordPiece tokenizer driven by the HF tokenizer.json
+// blob stored in the GGUF ("blob.tokenizer.json", reference bert.cpp:576-577).
+//
+// Replaces tokenizers-cpp@e47442f (Rust HF `tokenizers` behind a C++ shim,
+// reference tokenizer.cpp:30-53; un-vendored, needs rustc) for the pipeline BERT
+// checkpoints use: BertNormalizer (clean_text, handle_chinese_chars,
+// strip_accents, lowercase) -> BertPreTokenizer (whitespace + punctuation
+// split) -> WordPiece (greedy longest-match, "##" continuation,
+// max_input_chars_per_word) -> truncation / padding from the JSON.
+// Encode() returns content ids only (no [CLS]/[SEP]); bert_tokenize adds them,
+// exactly like the reference (bert.cpp:738-781).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace bertamd {
+
+class WordPieceTokenizer {
+public:
+    bool load(const std::string &json, std::string &err);
+    std::vector<int32_t> encode(const std::string &text) const;
+    bool loaded() const { return !vocab_.empty(); }
+
+    // exposed for tests
+    std::string normalize(const std::string &text) const;
+    std::vector<std::string> pre_tokenize(const std::string &normalized) const;
+
+private:
+    std::unordered_map<std::string, int32_t> vocab_;
+    std::string prefix_ = "##";
+    std::string unk_ = "[UNK]";
+    int max_chars_ = 100;
+    bool clean_text_ = true, chinese_ = true, lowercase_ = true;
+    int strip_accents_ = -1;  // -1: follow lowercase (BERT default)
+    int trunc_max_ = -1;      // content-token truncation (Encode without special tokens)
+    int pad_len_ = -1;        // fixed padding length, -1 = none
+    int32_t pad_id_ = 0;
+    // added (special) tokens are matched verbatim before normalisation
+    std::vector<std::pair<std::string, int32_t>> added_;
+};
+
+}  // namespace bertamd

@@ -1,0 +1,80 @@
+/*
+ * bert_amd.h — additive extensions of the drop-in library (not in the
+ * reference ABI; the reference consumers never need them).
+ *
+ * They exist for three callers:
+ *   - bench.py / tests: device-resident batch evaluation on a caller-chosen
+ *     HIP stream (inputs already in HBM, nothing copied, no sync);
+ *   - multi-GPU: choose the devices a context is replicated on (the
+ *     reference ABI has no device argument; SURVEY.md §8(b) "No device
+ *     argument");
+ *   - tooling: the deterministic synthetic GGUF generator and per-kernel
+ *     timing.
+ * All functions are C-ABI, take plain pointers and sizes, never throw, and
+ * return 0 on success / negative on error (message via bert_amd_last_error).
+ */
+#ifndef BERT_AMD_H
+#define BERT_AMD_H
+
+#include <stdint.h>
+
+#include "bert.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Load a GGUF and replicate its weights on the given HIP devices (ordinals as
+   seen by this process).  n_devices <= 0: all visible devices, or the list in
+   env BERT_AMD_DEVICES="0,1,...".  Returns NULL on error. */
+BERT_API struct bert_ctx *bert_amd_load(const char *fname, const int32_t *devices, int32_t n_devices);
+
+BERT_API int32_t bert_amd_n_devices(struct bert_ctx *ctx);
+
+/* hparams: [n_vocab, n_max_tokens, n_embd, n_intermediate, n_head, n_layer, weight ggml type] */
+BERT_API int32_t bert_amd_hparams(struct bert_ctx *ctx, int32_t *out7);
+
+/* Device-resident evaluation on replica `slot` (index into the context's
+   device list), enqueued on `hip_stream` (a hipStream_t; NULL = the
+   library's own stream for that device).  Asynchronous: returns after
+   enqueueing.
+     d_tokens   : int32, packed token ids of all sentences (device memory)
+     d_offsets  : int32[n_seqs+1], prefix offsets into d_tokens (device memory)
+     h_offsets  : the same offsets in host memory (used for grid sizing)
+     d_out      : float[n_seqs * n_embd] (device memory), L2-normalised
+   Workspace is grown on demand (allocation happens outside any capture when
+   the caller warms up with the largest batch first). */
+BERT_API int32_t bert_amd_eval_device(struct bert_ctx *ctx, int32_t slot, const int32_t *d_tokens,
+                                      const int32_t *d_offsets, const int32_t *h_offsets, int32_t n_seqs,
+                                      float *d_out, void *hip_stream);
+
+/* Per-kernel-class timing with HIP events on the launch stream.
+   enable != 0 turns it on for subsequent evals (adds event records between
+   launches; never used inside bench.py's timed region). */
+BERT_API int32_t bert_amd_profile_enable(struct bert_ctx *ctx, int32_t enable);
+/* Copies up to max_entries: names (NUL-separated into names_buf), total ms
+   and launch counts since enable.  Returns the number of entries. */
+BERT_API int32_t bert_amd_profile_read(struct bert_ctx *ctx, char *names_buf, int32_t names_len, float *total_ms,
+                                       int32_t *counts, int32_t max_entries);
+
+/* Deterministic synthetic BERT GGUF (see csrc/synth.cpp).
+   ftype: 0 = f32, 1 = f16, 2 = Q4_0, 3 = Q4_1 (2-D *.weight tensors). */
+BERT_API int bert_amd_synth_model(const char *path, int32_t n_vocab, int32_t n_max_tokens, int32_t n_embd,
+                                  int32_t n_intermediate, int32_t n_head, int32_t n_layer, int32_t ftype,
+                                  uint64_t seed, float w_std);
+
+/* Tokenizer without a model/GPU (tests, tooling): runs the native WordPiece
+   tokenizer configured by an HF tokenizer.json string.  frame == 0: the content
+   ids of Encode(text) (at most n_max_tokens); frame != 0: bert_tokenize's
+   [CLS] ... [SEP] framing with the given special ids.  Returns the count. */
+BERT_API int32_t bert_amd_tokenize_json(const char *tokenizer_json, const char *text, int32_t *tokens,
+                                        int32_t n_max_tokens, int32_t frame, int32_t cls_id, int32_t sep_id,
+                                        int32_t pad_id);
+
+BERT_API const char *bert_amd_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BERT_AMD_H */

@@ -1,0 +1,124 @@
+"""Generate the committed golden fixtures tests/golden/*.npz (test infrastructure).
+
+For every case: write the deterministic synthetic GGUF (bertlib.synth_model,
+splitmix64-seeded), draw the token ids the way SURVEY.md §8(d) prescribes
+([CLS] + uniform ids in [1000, V) from splitmix64(20250117 + sentence) + [SEP]),
+and evaluate them with the CPU oracle (oracle/bert_oracle.c).  The fixture
+stores inputs, oracle outputs and the sha256 of the model file, so the GPU
+tests can regenerate the same model on the box and prove it is byte-identical
+before comparing.  The reference itself cannot be built or run here
+(DESIGN.md §5), so these vectors pin the GPU path to the oracle, and the
+oracle is pinned separately (tests/test_oracle.py).
+
+Run:  python tests/golden/make_golden.py [case ...]
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "embedding.cpp_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import bertlib  # noqa: E402
+
+SEED = 20250117
+
+# name -> (shape, ftype, w_std, sentence lengths)
+CASES = {
+    "c1_minilm_f32": ("minilm", "f32", 0.05, [16, 32, 7]),
+    "c2_minilm_f16": ("minilm", "f16", 0.05, [128, 128, 128, 128]),
+    "c3_minilm_q4_0": ("minilm", "q4_0", 0.05, [128, 128, 128, 128]),
+    "c3_minilm_q4_0_ragged": ("minilm", "q4_0", 0.05, [1, 2, 17, 64, 129, 300, 512]),
+    "minilm_q4_1": ("minilm", "q4_1", 0.05, [128, 40]),
+    "minilm_q4_0_std01": ("minilm", "q4_0", 0.1, [128, 60]),
+    "c4_e5_f16": ("e5-base", "f16", 0.05, [256, 256]),
+    "c5_bge_q4_1": ("bge-large", "q4_1", 0.05, [512, 512]),
+}
+
+
+def splitmix64(state: int):
+    state = (state + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = state
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return state, z ^ (z >> 31)
+
+
+def sentence(index: int, n: int, n_vocab: int) -> list[int]:
+    """[CLS] r_1 .. r_{n-2} [SEP]; r uniform in [1000, n_vocab) from splitmix64(SEED + index)."""
+    if n == 1:
+        return [101]
+    st = SEED + index
+    ids = [101]
+    for _ in range(n - 2):
+        st, z = splitmix64(st)
+        ids.append(1000 + z % (n_vocab - 1000))
+    return ids + [102]
+
+
+def sha256(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 22), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def model_path(d: str, shape: str, ftype: str, w_std: float) -> str:
+    return os.path.join(d, f"{shape}_{ftype}_s{SEED}_w{w_std:g}.gguf")
+
+
+def ensure_model(d: str, shape: str, ftype: str, w_std: float) -> str:
+    p = model_path(d, shape, ftype, w_std)
+    if not os.path.exists(p):
+        bertlib.synth_model(p, shape, ftype, seed=SEED, w_std=w_std)
+    return p
+
+
+def load_case(name: str):
+    z = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    offs = z["offsets"]
+    toks = [z["tokens"][offs[i]:offs[i + 1]].tolist() for i in range(len(offs) - 1)]
+    return meta, toks, z["emb"]
+
+
+def make(name: str, model_dir: str):
+    import oracle  # test infrastructure only
+
+    shape, ftype, w_std, lens = CASES[name]
+    hp = bertlib.SHAPES[shape]
+    path = ensure_model(model_dir, shape, ftype, w_std)
+    toks = [sentence(i, n, hp["n_vocab"]) for i, n in enumerate(lens)]
+    t0 = time.time()
+    emb = oracle.Oracle(path).eval_batch(toks, 0)
+    dt = time.time() - t0
+    offs = np.zeros(len(toks) + 1, np.int32)
+    offs[1:] = np.cumsum([len(t) for t in toks])
+    meta = dict(case=name, shape=shape, hparams=hp, ftype=ftype, seed=SEED, w_std=w_std, lengths=lens,
+                model_sha256=sha256(path), oracle_seconds=round(dt, 2),
+                generator="bertlib.synth_model (csrc/synth.cpp)", oracle="oracle/bert_oracle.c")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), tokens=np.concatenate(toks).astype(np.int32),
+                        offsets=offs, emb=emb.astype(np.float32), meta=np.array(json.dumps(meta)))
+    print(f"{name}: {len(toks)} sentences, oracle {dt:.1f}s", flush=True)
+
+
+def main():
+    names = sys.argv[1:] or list(CASES)
+    model_dir = os.environ.get("BERT_AMD_MODEL_DIR") or os.path.join(tempfile.gettempdir(), "bert_amd_models")
+    os.makedirs(model_dir, exist_ok=True)
+    for n in names:
+        make(n, model_dir)
+
+
+if __name__ == "__main__":
+    main()
