@@ -30,10 +30,14 @@ enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3 };
 struct ActPtr {
     void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K]
     void *d = nullptr;  // per-32-block scale [M][K/32]: fp16 (Q8_0) | f32 (Q8_1)
+    void *s = nullptr;  // Q8_1 only: d * sum(q) per block, f32 [M][K/32]
 };
 
 // Weights repacked at load time into MFMA fragment order:
-//   per (16-row n-tile, 32-wide k-block) one 64-lane fragment.
+//   per (16-row n-tile, 32-wide k-block) one 64-lane fragment.  Output
+//   columns are interleaved in pairs of n-tiles: repacked tile 2p+t, lane
+//   column c holds weight row 32p + 2c + t, so after the MFMA each lane owns two
+//   ADJACENT output columns (vectorised epilogue stores, in-register Q8 blocks).
 //   Q4_x: q = u32 [N/16][K/32][64] (8 nibbles per lane), d (and m) = fp16 [N/16][K/32][16]
 //   F16 : q = fp16 [N/16][K/32][64][8]
 //   F32 : q = f32  [N/16][K/32][64][8]

@@ -174,8 +174,14 @@ struct Packed {
     std::vector<uint8_t> q, d, m;
 };
 
-Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows, int64_t K) {
-    const int64_t N = (int64_t)rows.size(), nkb = K / 32, ntl = N / 16;
+Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_t K) {
+    const int64_t N = (int64_t)rows_in.size(), nkb = K / 32, ntl = N / 16;
+    // column interleave (kernels.h WPtr): repacked tile 2p+t, lane column c
+    // <- weight row 32p + 2c + t, i.e. repacked row 16*(2p+t) + c
+    std::vector<const uint8_t *> rows((size_t)N);
+    for (int64_t pr = 0; pr < N / 32; pr++)
+        for (int t = 0; t < 2; t++)
+            for (int c = 0; c < 16; c++) rows[(size_t)(32 * pr + 16 * t + c)] = rows_in[(size_t)(32 * pr + 2 * c + t)];
     Packed p;
     if (type == GT_Q4_0 || type == GT_Q4_1) {
         const int bs = type == GT_Q4_0 ? 18 : 20, qoff = type == GT_Q4_0 ? 2 : 4;
@@ -255,6 +261,7 @@ bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, i
     if (!dmalloc(track, &a.q, (size_t)rows * K * act_elem_bytes(wtype))) return false;
     if (act_scale_bytes(wtype) && !dmalloc(track, &a.d, (size_t)rows * (K / 32) * act_scale_bytes(wtype)))
         return false;
+    if (wtype == W_Q4_1 && !dmalloc(track, &a.s, (size_t)rows * (K / 32) * 4)) return false;
     return true;
 }
 

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import bertlib
-from make_golden import CASES, SEED, ensure_model, load_case, sentence, sha256
+from make_golden import CASES, CHAOTIC, SEED, ensure_model, load_case, sentence, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -29,10 +29,13 @@ def cos(a, b):
 _models = {}
 
 
-def get_model(model_dir, shape, ftype, w_std=0.05):
-    key = (shape, ftype, w_std)
+def get_model(model_dir, shape, ftype, w_std=0.05, n_layer=None):
+    key = (shape, ftype, w_std, n_layer)
     if key not in _models:
-        p = ensure_model(model_dir, shape, ftype, w_std)
+        for k in list(_models):  # keep at most one big model resident at a time
+            if k[0] != "minilm":
+                _models.pop(k)[1].close()
+        p = ensure_model(model_dir, shape, ftype, w_std, n_layer)
         _models[key] = (p, bertlib.BertModel(p))
     return _models[key]
 
@@ -48,14 +51,20 @@ def _cleanup():
 @pytest.mark.parametrize("case", list(CASES))
 def test_golden_vectors(case, model_dir):
     meta, toks, want = load_case(case)
-    p, m = get_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"])
+    p, m = get_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
     assert sha256(p) == meta["model_sha256"], "generator is not reproducing the fixture's model on this host"
     got = m.eval_batch(toks)
     assert np.all(np.isfinite(got))
     c = cos(got, want)
     print(f"{case}: 1-cos min/mean {1 - c.max():.2e}/{1 - c.mean():.2e} max {1 - c.min():.2e} "
           f"maxabs {np.abs(got - want).max():.2e}")
-    assert c.min() >= COS_TOL, (case, 1 - c)
+    if case in CHAOTIC:
+        # intrinsic sensitivity: an exact float64 restatement lands this far from the
+        # oracle; the GPU must not be further than twice that (and never NaN/garbage)
+        bound = np.maximum(2.0 * np.asarray(meta["exact_restatement_1mcos"]), 1 - COS_TOL)
+        assert np.all(1 - c <= bound), (case, 1 - c, bound)
+    else:
+        assert c.min() >= COS_TOL, (case, 1 - c)
     assert np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-5)
 
 
