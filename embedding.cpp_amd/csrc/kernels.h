@@ -30,24 +30,44 @@ enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3 };
 struct ActPtr {
     void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K]
     void *d = nullptr;  // per-32-block scale [M][K/32]: fp16 (Q8_0) | f32 (Q8_1)
-    void *s = nullptr;  // Q8_1 only: d * sum(q) per block, f32 [M][K/32]
 };
 
 // Weights repacked at load time into MFMA fragment order:
-//   per (16-row n-tile, 32-wide k-block) one 64-lane fragment.  Output
-//   columns are interleaved in pairs of n-tiles: repacked tile 2p+t, lane
-//   column c holds weight row 32p + 2c + t, so after the MFMA each lane owns two
-//   ADJACENT output columns (vectorised epilogue stores, in-register Q8 blocks).
-//   Q4_x: q = u32 [N/16][K/32][64] (8 nibbles per lane), d (and m) = fp16 [N/16][K/32][16]
+//   per (16-row n-tile, 32-wide k-block) one 64-lane fragment; lane l holds
+//   row (l & 15), k = 8(l >> 4) .. +7.  Output columns are interleaved in pairs
+//   of n-tiles: repacked tile 2p+t, lane column c holds weight row 32p + 2c + t,
+//   so after the MFMA each lane owns two ADJACENT output columns (vectorised
+//   epilogue stores, in-register Q8 blocks).
+//   Q4_x: q = fp16 [N/16][K/32][2][64][8]: the dequantised weight w = d*(q-8)
+//         (Q4_0) or d*q + m (Q4_1), times 2^S, split as hi = fp16(w),
+//         lo = fp16(w - hi).  For Q4_0 the split is exact (w has <= 15
+//         significant bits), so an fp16 MFMA over integer Q8 activations
+//         returns d_w * sum(q_a * q_w) exactly in each product; `unscale` = 2^-S.
 //   F16 : q = fp16 [N/16][K/32][64][8]
 //   F32 : q = f32  [N/16][K/32][64][8]
 struct WPtr {
     const void *q = nullptr;
-    const void *d = nullptr;
-    const void *m = nullptr;
+    float unscale = 1.f;
 };
 
-enum Epi : int { EPI_BIAS_F32 = 0, EPI_GELU_ACT = 1, EPI_LN = 2 };
+enum Epi : int { EPI_QKV = 0, EPI_GELU_ACT = 1, EPI_LN = 2 };
+
+// Piecewise view of a 65536-entry fp16 -> fp16 table (ggml's GELU / exp
+// tables, built on the host with glibc exactly as ggml_init builds them) whose
+// non-trivial part fits LDS.  Entries for h in [0, pos_n) and
+// [0x8000, 0x8000 + neg_n) are stored compactly: compact[h] and
+// compact[pos_n + (h & 0x7fff)].  Beyond them the host has verified that the
+// table is h itself (pos_identity) or the constant neg_const; every other
+// pattern (inf / NaN, non-identity positives) reads `full` in global memory.
+constexpr int HALF_TABLE_LDS = 36864;  // max compact GELU entries (72 KiB of LDS)
+constexpr int EXP_TABLE_LDS = 20480;   // max compact exp entries (40 KiB of LDS)
+struct HalfTable {
+    const uint16_t *full = nullptr;
+    const uint16_t *compact = nullptr;  // n_pad entries, n_pad % 8 == 0
+    int pos_n = 0, neg_n = 0, n_pad = 0;
+    int pos_identity = 0;
+    uint32_t neg_const = 0;
+};
 
 struct GemmArgs {
     ActPtr A;              // [Mpad][K] in the activation format of wtype
@@ -55,12 +75,15 @@ struct GemmArgs {
     WPtr W;                // [N][K] repacked
     int N = 0;
     const float *bias = nullptr;   // [N]
-    float *out_f32 = nullptr;      // EPI_BIAS_F32: [Mpad][N]
+    // EPI_QKV: y = b + W.x (f32, as ggml), stored split for the attention MFMAs:
+    // Q | K as hi/lo fp16 planes [Mpad][2E], V transposed as hi/lo planes [E][ldv]
+    uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16 bits
+    int64_t ldv = 0;
     ActPtr out_act;                // EPI_GELU_ACT: [Mpad][N]; EPI_LN: [Mpad][N]
     float *X = nullptr;            // EPI_LN: residual in / LN out, f32 [Mpad][N]
     const float *ln_w = nullptr, *ln_b = nullptr;
     float eps = 0.f;
-    const uint16_t *gelu_tab = nullptr;  // fp16 -> fp16 table (ggml_init, host-built)
+    HalfTable gelu;                      // EPI_GELU_ACT: ggml's fp16 GELU table
 };
 
 struct EmbedArgs {
@@ -76,15 +99,17 @@ struct EmbedArgs {
 };
 
 struct AttnArgs {
-    const float *qkv = nullptr;        // [Mpad][3E]: Q | K | V
+    const uint16_t *qk_hi = nullptr, *qk_lo = nullptr;  // fp16 [Mpad][2E]: Q | K (GemmArgs EPI_QKV)
+    const uint16_t *vt_hi = nullptr, *vt_lo = nullptr;  // fp16 [E][ldv]: V^T
+    int64_t ldv = 0;
     const int32_t *offsets = nullptr;
     int E = 0, H = 0;
     float scale = 0.f;                 // 1.0f / sqrtf(d_head)
-    const uint16_t *exp_tab = nullptr; // fp16 -> fp16 exp table
+    HalfTable expt;                    // ggml's fp16 exp table
     ActPtr ctx;                        // [Mpad][E] activation format
 };
 
-constexpr int GEMM_BM = 64;   // rows per GEMM workgroup
+constexpr int GEMM_BM = 128;  // M padding unit = the largest GEMM row tile
 constexpr int ATT_QB = 64;    // queries per attention workgroup
 
 // Launchers (kernels.hip).  Return hipSuccess or the launch error.

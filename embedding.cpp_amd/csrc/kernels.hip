@@ -11,6 +11,8 @@
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace bertamd {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -20,7 +22,7 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 typedef float float16v __attribute__((ext_vector_type(16)));
 typedef _Float16 half4v __attribute__((ext_vector_type(4)));
 
-constexpr int BM_MAX = GEMM_BM;  // M padding unit; GEMM tiles use BM = 64 or 32
+constexpr int BM_MAX = GEMM_BM;  // M padding unit; GEMM tiles use BM = 128, 64 or 32
 constexpr int KC = 64;       // K per main-loop chunk = two 32-element quant blocks
 constexpr int LDA_H = 80;    // fp16 A-tile row stride (halves) = 160 B: ds_read_b128 conflict-free
 constexpr int LDA_F = 72;    // f32  A-tile row stride (floats) = 288 B: ds_read_b128 conflict-free
@@ -41,14 +43,12 @@ __device__ __forceinline__ void store_act_block(const ActPtr &A, int64_t ld, int
         const float d = amax / 127.f;
         const float id = amax != 0.f ? 127.f / amax : 0.f;
         uint32_t pk[8];
-        int qsum = 0;
 #pragma unroll
         for (int w = 0; w < 8; w++) {
             uint32_t x = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int q = (int)rintf(v[4 * w + j] * id);
-                qsum += q;
                 x |= ((uint32_t)(q & 0xff)) << (8 * j);
             }
             pk[w] = x;
@@ -59,8 +59,7 @@ __device__ __forceinline__ void store_act_block(const ActPtr &A, int64_t ld, int
         if constexpr (WT == W_Q4_0) {
             ((uint16_t *)A.d)[row * (ld / 32) + blk] = f2h(d);
         } else {
-            ((float *)A.d)[row * (ld / 32) + blk] = d;
-            ((float *)A.s)[row * (ld / 32) + blk] = d * (float)qsum;  // quantize_row_q8_1: s = d * sum(q)
+            ((float *)A.d)[row * (ld / 32) + blk] = d;  // Q8_1's s = d*sum(q) is not needed: m_w is in the split W
         }
     } else if constexpr (WT == W_F16) {
         half8 *dst = (half8 *)((_Float16 *)A.q + row * ld + blk * 32);
@@ -76,6 +75,61 @@ __device__ __forceinline__ void store_act_block(const ActPtr &A, int64_t ld, int
 #pragma unroll
         for (int w = 0; w < 8; w++) dst[w] = float4v{v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3]};
     }
+}
+
+// The same for one quarter (8 elements) of a block: the four quarters of a
+// block are four adjacent lanes (t & 3), all active; the block's amax is
+// combined with two xor-shuffles, so each lane needs only its own 8 values.
+template <int WT>
+__device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, int64_t row, int blk, int qq,
+                                                  const float *v) {
+    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
+        amax = fmaxf(amax, __shfl_xor(amax, 1));
+        amax = fmaxf(amax, __shfl_xor(amax, 2));
+        const float d = amax / 127.f;
+        const float id = amax != 0.f ? 127.f / amax : 0.f;
+        uint32_t pk[2];
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int q = (int)rintf(v[4 * w + j] * id);
+                x |= ((uint32_t)(q & 0xff)) << (8 * j);
+            }
+            pk[w] = x;
+        }
+        *(uint2 *)((int8_t *)A.q + row * ld + blk * 32 + 8 * qq) = make_uint2(pk[0], pk[1]);
+        if (qq == 0) {
+            if constexpr (WT == W_Q4_0)
+                ((uint16_t *)A.d)[row * (ld / 32) + blk] = f2h(d);
+            else
+                ((float *)A.d)[row * (ld / 32) + blk] = d;
+        }
+    } else if constexpr (WT == W_F16) {
+        half8 h;
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = (_Float16)v[j];
+        *(half8 *)((_Float16 *)A.q + row * ld + blk * 32 + 8 * qq) = h;
+    } else {
+        float4v *dst = (float4v *)((float *)A.q + row * ld + blk * 32 + 8 * qq);
+        dst[0] = float4v{v[0], v[1], v[2], v[3]};
+        dst[1] = float4v{v[4], v[5], v[6], v[7]};
+    }
+}
+
+// fp16 -> fp16 table lookup through the LDS-resident compact part (kernels.h HalfTable).
+__device__ __forceinline__ uint32_t half_table(const uint16_t *lds, const HalfTable &T, uint32_t h) {
+    const uint32_t mag = h & 0x7fffu;
+    const bool neg = (h & 0x8000u) != 0;
+    const bool in = neg ? mag < (uint32_t)T.neg_n : mag < (uint32_t)T.pos_n;
+    const uint32_t v = lds[in ? (neg ? T.pos_n + mag : mag) : 0];
+    uint32_t r = in ? v : (neg ? T.neg_const : h);
+    if (__builtin_expect(mag >= 0x7c00u || (!neg && !in && !T.pos_identity), 0)) r = T.full[h];
+    return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -143,23 +197,26 @@ __device__ void ln_row_phase(float *stage, int ld, int ncols, double *red, int64
     __syncthreads();
 }
 
-// LayerNorm row phase for GEMM slices: task t -> (block b = t / 16, row r = t % 16),
-// v = (bias + acc) + x, two-pass double statistics combined in a fixed block order.
+// LayerNorm row phase for GEMM slices, four lanes per (row, 32-column block):
+// task t -> quarter qq = t & 3, block b, row r.  v = (bias + acc) + x; two-pass
+// statistics in double (ggml_norm), combined quarter -> block (two shuffles)
+// -> row (fixed block order); then y = w * (v * scale) + b, stored to X and in
+// the next matmul's activation format.
 template <int WT, int NBLK>
-__device__ void ln_row_phase_t(float *stage, int ld, double *red, int64_t row0, const float *__restrict__ bias,
+__device__ void ln_row_phase_q(float *stage, int ld, double *red, int64_t row0, const float *__restrict__ bias,
                                float *X, const float *__restrict__ lnw, const float *__restrict__ lnb, float eps,
                                const ActPtr &out, int tid, int nthreads) {
-    constexpr int ncols = NBLK * 32, ntask = 16 * NBLK;
-    double *red1 = red, *red2 = red + ntask;
+    constexpr int ncols = NBLK * 32, ntask = 64 * NBLK;
+    double *red1 = red, *red2 = red + 16 * NBLK;
     for (int t = tid; t < ntask; t += nthreads) {
-        const int b = t >> 4, r = t & 15;
-        float *sp = stage + r * ld + 32 * b;
-        const float *xr = X + (row0 + r) * (int64_t)ncols + 32 * b;
+        const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+        float *sp = stage + r * ld + c;
+        const float *xr = X + (row0 + r) * (int64_t)ncols + c;
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < 2; k++) {
             float4v v = *(float4v *)(sp + 4 * k);
-            const float4v bb = *(const float4v *)(bias + 32 * b + 4 * k);
+            const float4v bb = *(const float4v *)(bias + c + 4 * k);
             const float4v x = *(const float4v *)(xr + 4 * k);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -168,19 +225,21 @@ __device__ void ln_row_phase_t(float *stage, int ld, double *red, int64_t row0, 
             }
             *(float4v *)(sp + 4 * k) = v;
         }
-        red1[r * NBLK + b] = s;
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        if (qq == 0) red1[r * NBLK + b] = s;
     }
     __syncthreads();
     for (int t = tid; t < ntask; t += nthreads) {
-        const int b = t >> 4, r = t & 15;
+        const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
         double tot = 0.0;
 #pragma unroll
         for (int k = 0; k < NBLK; k++) tot += red1[r * NBLK + k];
         const float mean = (float)(tot / ncols);
-        float *sp = stage + r * ld + 32 * b;
+        float *sp = stage + r * ld + c;
         double s2 = 0.0;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < 2; k++) {
             float4v v = *(float4v *)(sp + 4 * k);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -189,23 +248,25 @@ __device__ void ln_row_phase_t(float *stage, int ld, double *red, int64_t row0, 
             }
             *(float4v *)(sp + 4 * k) = v;
         }
-        red2[r * NBLK + b] = s2;
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        if (qq == 0) red2[r * NBLK + b] = s2;
     }
     __syncthreads();
     for (int t = tid; t < ntask; t += nthreads) {
-        const int b = t >> 4, r = t & 15;
+        const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
         double tot = 0.0;
 #pragma unroll
         for (int k = 0; k < NBLK; k++) tot += red2[r * NBLK + k];
         const float var = (float)(tot / ncols);
         const float scale = 1.0f / sqrtf(var + eps);
-        const float *sp = stage + r * ld + 32 * b;
-        float y[32];
+        const float *sp = stage + r * ld + c;
+        float y[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < 2; k++) {
             const float4v v = *(const float4v *)(sp + 4 * k);
-            const float4v w = *(const float4v *)(lnw + 32 * b + 4 * k);
-            const float4v bb = *(const float4v *)(lnb + 32 * b + 4 * k);
+            const float4v w = *(const float4v *)(lnw + c + 4 * k);
+            const float4v bb = *(const float4v *)(lnb + c + 4 * k);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 float z = v[j] * scale;
@@ -213,10 +274,10 @@ __device__ void ln_row_phase_t(float *stage, int ld, double *red, int64_t row0, 
                 y[4 * k + j] = z + bb[j];
             }
         }
-        float4v *xo = (float4v *)(X + (row0 + r) * (int64_t)ncols + 32 * b);
-#pragma unroll
-        for (int k = 0; k < 8; k++) xo[k] = float4v{y[4 * k], y[4 * k + 1], y[4 * k + 2], y[4 * k + 3]};
-        store_act_block<WT>(out, ncols, row0 + r, b, y);
+        float4v *xo = (float4v *)(X + (row0 + r) * (int64_t)ncols + c);
+        xo[0] = float4v{y[0], y[1], y[2], y[3]};
+        xo[1] = float4v{y[4], y[5], y[6], y[7]};
+        store_act_quarter<WT>(out, ncols, row0 + r, b, qq, y);
     }
 }
 
@@ -310,7 +371,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
 // that coalesce into whole rows.
 struct AReg {
     uint4 r[4];
-    float d, s;
+    float d;
 };
 
 template <int WT>
@@ -325,7 +386,6 @@ __device__ __forceinline__ void a_load(AReg &ar, const ActPtr &A, int K, int64_t
             ar.d = h2f(((const uint16_t *)A.d)[bi]);
         } else {
             ar.d = ((const float *)A.d)[bi];
-            ar.s = ((const float *)A.s)[bi];
         }
     } else if constexpr (WT == W_F16) {
         const uint4 *p = (const uint4 *)((const uint16_t *)A.q + row * K + k);
@@ -351,7 +411,7 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t x, half2v &lo, half2v &hi) 
 }
 
 template <int WT, int BM>
-__device__ __forceinline__ void a_store(const AReg &ar, char *buf, int item) {
+__device__ __forceinline__ void a_store(const AReg &ar, char *buf, int item, float unscale) {
     const int r = item >> 2, s = item & 3;
     constexpr int A_BYTES = (WT == W_F32) ? BM * LDA_F * 4 : BM * LDA_H * 2;
     if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
@@ -370,9 +430,8 @@ __device__ __forceinline__ void a_store(const AReg &ar, char *buf, int item) {
         dst[0] = h0;
         dst[1] = h1;
         if ((s & 1) == 0) {
-            float *sc = (float *)(buf + A_BYTES);  // [dA: 2][BM] then [sA: 2][BM]
-            sc[(s >> 1) * BM + r] = ar.d;
-            if constexpr (WT == W_Q4_1) sc[2 * BM + (s >> 1) * BM + r] = ar.s;
+            float *sc = (float *)(buf + A_BYTES);  // [block 0, 1 of the chunk][BM]: d_a * 2^-S (exact)
+            sc[(s >> 1) * BM + r] = ar.d * unscale;
         }
     } else if constexpr (WT == W_F16) {
         uint4 *dst = (uint4 *)((uint16_t *)buf + r * LDA_H + s * 16);
@@ -388,8 +447,8 @@ __device__ __forceinline__ void a_store(const AReg &ar, char *buf, int item) {
 }
 
 template <int WT> struct WFrag;
-template <> struct WFrag<W_Q4_0> { uint32_t q; _Float16 d; };
-template <> struct WFrag<W_Q4_1> { uint32_t q; _Float16 d, m; };
+template <> struct WFrag<W_Q4_0> { half8 hi, lo; };
+template <> struct WFrag<W_Q4_1> { half8 hi, lo; };
 template <> struct WFrag<W_F16> { half8 h; };
 template <> struct WFrag<W_F32> { float4v f[2]; };
 
@@ -398,9 +457,8 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
     const int lane = threadIdx.x & 63;
     WFrag<WT> f;
     if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
-        f.q = ((const uint32_t *)W.q)[tile * 64 + lane];
-        f.d = ((const _Float16 *)W.d)[tile * 16 + (lane & 15)];
-        if constexpr (WT == W_Q4_1) f.m = ((const _Float16 *)W.m)[tile * 16 + (lane & 15)];
+        f.hi = ((const half8 *)W.q)[(tile * 2) * 64 + lane];
+        f.lo = ((const half8 *)W.q)[(tile * 2 + 1) * 64 + lane];
     } else if constexpr (WT == W_F16) {
         f.h = ((const half8 *)W.q)[tile * 64 + lane];
     } else {
@@ -408,24 +466,6 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
         f.f[1] = ((const float4v *)W.q)[(tile * 64 + lane) * 2 + 1];
     }
     return f;
-}
-
-// 8 nibbles -> 8 exact fp16 integers (q-8 for Q4_0, q for Q4_1).  Nibble slot s
-// holds fragment element 2s (s<4) or 2(s-4)+1 (s>=4), so (x >> 4j) & 0x000F000F
-// yields elements (2j, 2j+1); 0x6400|q is the fp16 value 1024+q.
-template <int WT>
-__device__ __forceinline__ half8 w_int(uint32_t x) {
-    half8 r;
-    const _Float16 o = (WT == W_Q4_0) ? (_Float16)1032.f : (_Float16)1024.f;
-    const half2v off = {o, o};
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t w = ((x >> (4 * j)) & 0x000F000Fu) | 0x64006400u;
-        const half2v h = __builtin_bit_cast(half2v, w) - off;
-        r[2 * j] = h[0];
-        r[2 * j + 1] = h[1];
-    }
-    return r;
 }
 
 template <int WT, int EPI, int BN, int NW, int BM>
@@ -438,11 +478,15 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
-    constexpr int A_BUF = A_BYTES + (QP ? 4 * BM * 4 : 0);
-    constexpr int EPI_LDS = (EPI == EPI_BIAS_F32) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
+    constexpr int A_BUF = A_BYTES + (QP ? 2 * BM * 4 : 0);
+    constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
+    constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
+    constexpr int EPI_LDS = (EPI == EPI_QKV) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
+    static_assert(EPI == EPI_QKV || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
+    __shared__ __attribute__((aligned(16))) uint16_t gtab[EPI == EPI_GELU_ACT ? HALF_TABLE_LDS : 8];
 
     // XCD-aware tile order: linear block ids are dealt round-robin over the 8
     // XCDs; remap so that each XCD walks a contiguous range, n fastest, so the
@@ -458,6 +502,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     const int n0 = ntile * BN;
     const int K = args.K, nkc = K / KC, nkb = K >> 5;
     const int64_t ntile0 = (n0 + wv * WN) >> 4;
+    const float unscale = args.W.unscale;
+    if constexpr (EPI == EPI_GELU_ACT) {  // GELU table -> LDS (read after the main loop's barriers)
+        for (int i = tid; i < args.gelu.n_pad / 8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.compact)[i];
+    }
 
     float4v acc[RT][NTW];
 #pragma unroll
@@ -465,13 +513,18 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
 #pragma unroll
         for (int j = 0; j < NTW; j++) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-    AReg ar;
-    const bool stager = tid < BM * (KC / 16);
-    if (stager) {
-        a_load<WT>(ar, args.A, K, m0, 0, tid);
-        a_store<WT, BM>(ar, smem, tid);
+    AReg ar[IT];
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+        const int item = tid + it * NT;
+        if (item < ITEMS) {
+            a_load<WT>(ar[it], args.A, K, m0, 0, item);
+            a_store<WT, BM>(ar[it], smem, item, unscale);
+        }
     }
-    WFrag<WT> wf[F32P ? 1 : 2][NTW], wn[F32P ? 1 : 2][NTW];
+    // W fragments of the two blocks in flight: block b lives in wf[b & 1] and
+    // is replaced by block b + 2 as soon as its MFMAs are issued
+    WFrag<WT> wf[F32P ? 1 : 2][NTW];
     if constexpr (!F32P) {
 #pragma unroll
         for (int kb = 0; kb < 2; kb++)
@@ -483,63 +536,61 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     const float4v zero4 = {0.f, 0.f, 0.f, 0.f};
     for (int kc = 0; kc < nkc; kc++) {
         const bool more = kc + 1 < nkc;
-        if (stager && more) a_load<WT>(ar, args.A, K, m0, (kc + 1) * KC, tid);
-        if constexpr (!F32P) {
-            if (more) {
+        if (more) {
 #pragma unroll
-                for (int kb = 0; kb < 2; kb++)
-#pragma unroll
-                    for (int nt = 0; nt < NTW; nt++)
-                        wn[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + (kc + 1) * 2 + kb);
+            for (int it = 0; it < IT; it++) {
+                const int item = tid + it * NT;
+                if (item < ITEMS) a_load<WT>(ar[it], args.A, K, m0, (kc + 1) * KC, item);
             }
         }
         const char *abuf = smem + (kc & 1) * A_BUF;
 #pragma unroll
         for (int kb = 0; kb < 2; kb++) {
             if constexpr (QP) {
-                half8 a[RT];
-                float4v da[RT], sa[RT];
-                const float *sc = (const float *)(abuf + A_BYTES);
-#pragma unroll
-                for (int rt = 0; rt < RT; rt++) {
-                    a[rt] = *(const half8 *)((const _Float16 *)abuf + (rt * 16 + c16) * LDA_H + kb * 32 + 8 * g);
-                    da[rt] = *(const float4v *)(sc + kb * BM + rt * 16 + g * 4);
-                    if constexpr (WT == W_Q4_1) sa[rt] = *(const float4v *)(sc + 2 * BM + kb * BM + rt * 16 + g * 4);
-                }
-                half8 b[NTW];
-                float dw[NTW], mw[NTW];
-#pragma unroll
-                for (int nt = 0; nt < NTW; nt++) {
-                    b[nt] = w_int<WT>(wf[kb][nt].q);
-                    dw[nt] = (float)wf[kb][nt].d;
-                    if constexpr (WT == W_Q4_1) mw[nt] = (float)wf[kb][nt].m;
-                }
-                // software pipeline: MFMA of tile t+1 in flight while tile t's
-                // integer sum is folded in (keeps two block sums live, not RT*NTW)
+                // Per (row tile, n-tile): blk = A.hi + A.lo  (two MFMAs: the exact
+                // d_w-scaled block dot product, f32-accumulated), then ONE fma
+                // folds it in with the row's d_a:  acc = fma(d_a * 2^-S, blk, acc).
+                // Software-pipelined: tile t+1's MFMA pair is in flight while
+                // tile t is folded; A fragments are read from LDS two tiles ahead.
                 constexpr int T = RT * NTW;
+                const float *sc = (const float *)(abuf + A_BYTES) + kb * BM;
+                half8 a[RT];
+                float4v da[RT];
+                auto lds_a = [&](int rt) {
+                    a[rt] = *(const half8 *)((const _Float16 *)abuf + (rt * 16 + c16) * LDA_H + kb * 32 + 8 * g);
+                    da[rt] = *(const float4v *)(sc + rt * 16 + g * 4);
+                };
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++)
+                    if (rt * NTW <= 1) lds_a(rt);
                 float4v blk[2];
-                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], zero4, 0, 0, 0);
+                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb][0].hi, zero4, 0, 0, 0);
+                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb][0].lo, blk[0], 0, 0, 0);
 #pragma unroll
                 for (int t = 0; t < T; t++) {
-                    if (t + 1 < T)
-                        blk[(t + 1) & 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[(t + 1) % RT], b[(t + 1) / RT],
-                                                                                   zero4, 0, 0, 0);
-                    const int rt = t % RT, nt = t / RT;
 #pragma unroll
-                    for (int i = 0; i < 4; i += 2) {  // packed f32: two rows per instruction
-                        const float2v dw2 = {dw[nt], dw[nt]};
-                        const float2v sc2 = float2v{da[rt][i], da[rt][i + 1]} * dw2;  // exact: fp16 x fp16
-                        float2v a2 = {acc[rt][nt][i], acc[rt][nt][i + 1]};
-                        a2 = __builtin_elementwise_fma(sc2, float2v{blk[t & 1][i], blk[t & 1][i + 1]}, a2);
-                        if constexpr (WT == W_Q4_1) {
-                            const float2v mw2 = {mw[nt], mw[nt]};
-                            a2 = __builtin_elementwise_fma(mw2, float2v{sa[rt][i], sa[rt][i + 1]}, a2);
-                        }
-                        asm volatile("" : "+v"(a2));  // keep the fold here (no sinking past MFMAs)
-                        acc[rt][nt][i] = a2[0];
-                        acc[rt][nt][i + 1] = a2[1];
+                    for (int rt = 0; rt < RT; rt++)
+                        if (rt * NTW == t + 2) lds_a(rt);
+                    if (t + 1 < T) {
+                        const int rt1 = (t + 1) / NTW, nt1 = (t + 1) % NTW;
+                        blk[(t + 1) & 1] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb][nt1].hi, zero4, 0, 0, 0);
+                        blk[(t + 1) & 1] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb][nt1].lo, blk[(t + 1) & 1], 0, 0, 0);
+                    }
+                    const int rt = t / NTW, nt = t % NTW;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        float v = acc[rt][nt][i];
+                        v = __builtin_fmaf(da[rt][i], blk[t & 1][i], v);
+                        asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
+                        acc[rt][nt][i] = v;
                     }
                     __builtin_amdgcn_sched_barrier(0);
+                }
+                if (more) {
+#pragma unroll
+                    for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + (kc + 1) * 2 + kb);
                 }
             } else if constexpr (WT == W_F16) {
                 half8 a[RT];
@@ -551,6 +602,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
 #pragma unroll
                     for (int rt = 0; rt < RT; rt++)
                         acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb][nt].h, acc[rt][nt], 0, 0, 0);
+                if (more) {
+#pragma unroll
+                    for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + (kc + 1) * 2 + kb);
+                }
             } else {
 #pragma unroll
                 for (int nt = 0; nt < NTW; nt++) wf[0][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * 2 + kb);
@@ -573,12 +628,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
             }
         }
         if (more) {
-            if (stager) a_store<WT, BM>(ar, smem + ((kc + 1) & 1) * A_BUF, tid);
-            if constexpr (!F32P) {
 #pragma unroll
-                for (int kb = 0; kb < 2; kb++)
-#pragma unroll
-                    for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = wn[kb][nt];
+            for (int it = 0; it < IT; it++) {
+                const int item = tid + it * NT;
+                if (item < ITEMS) a_store<WT, BM>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
         __syncthreads();
@@ -588,19 +641,45 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     //      row = m0 + rt*16 + 4g + i, columns col0 + {0, 1} with
     //      col0 = n0 + wv*WN + 32p + 2*c16; values acc[rt][2p][i], acc[rt][2p+1][i].
     const int colw = n0 + wv * WN + 2 * c16;
-    if constexpr (EPI == EPI_BIAS_F32) {
+    if constexpr (EPI == EPI_QKV) {
+        // y = b + W.x in f32 (ggml), split hi = fp16(y), lo = fp16(y - hi) for the
+        // attention MFMAs.  A column pair lies wholly in Q|K or in V (E % 32 == 0).
+        const int E = args.N / 3;
 #pragma unroll
         for (int p = 0; p < NP; p++) {
             const int col = colw + 32 * p;
             const float2v b = *(const float2v *)(args.bias + col);
+            if (col < 2 * E) {
 #pragma unroll
-            for (int rt = 0; rt < RT; rt++)
+                for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int64_t row = m0 + rt * 16 + 4 * g + i;
-                    *(float2v *)(args.out_f32 + row * args.N + col) =
-                        float2v{b[0] + acc[rt][2 * p][i], b[1] + acc[rt][2 * p + 1][i]};  // b + W.x
+                    for (int i = 0; i < 4; i++) {
+                        const int64_t row = m0 + rt * 16 + 4 * g + i;
+                        const float y0 = b[0] + acc[rt][2 * p][i], y1 = b[1] + acc[rt][2 * p + 1][i];
+                        const _Float16 h0 = (_Float16)y0, h1 = (_Float16)y1;
+                        *(half2v *)((_Float16 *)args.qk_hi + row * (2 * E) + col) = half2v{h0, h1};
+                        *(half2v *)((_Float16 *)args.qk_lo + row * (2 * E) + col) =
+                            half2v{(_Float16)(y0 - (float)h0), (_Float16)(y1 - (float)h1)};
+                    }
+            } else {
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++) {
+                    const int64_t row0 = m0 + rt * 16 + 4 * g;
+#pragma unroll
+                    for (int t = 0; t < 2; t++) {
+                        half4v hv, lv;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const float y = b[t] + acc[rt][2 * p + t][i];
+                            hv[i] = (_Float16)y;
+                            lv[i] = (_Float16)(y - (float)hv[i]);
+                        }
+                        const int64_t c = col + t - 2 * E;
+                        *(half4v *)((_Float16 *)args.vt_hi + c * args.ldv + row0) = hv;
+                        *(half4v *)((_Float16 *)args.vt_lo + c * args.ldv + row0) = lv;
+                    }
                 }
+            }
         }
     } else {
         // GELU / LayerNorm epilogues through a 16-row LDS slice: one thread per
@@ -621,24 +700,22 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
             __syncthreads();
             const int64_t row0 = m0 + rt * 16;
             if constexpr (EPI == EPI_GELU_ACT) {
-                for (int t = tid; t < 16 * NBLK; t += NT) {
-                    const int b = t >> 4, r = t & 15, col0 = n0 + 32 * b;
-                    const float *sp = stage + r * LD + 32 * b;
-                    float y[32];
-                    uint16_t hv[32];
+                // gelu(b + W.x) through ggml's fp16 table, four lanes per block
+                for (int t = tid; t < 64 * NBLK; t += NT) {
+                    const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+                    const float *sp = stage + r * LD + c;
+                    float y[8];
 #pragma unroll
-                    for (int k = 0; k < 8; k++) {
+                    for (int k = 0; k < 2; k++) {
                         const float4v v = *(const float4v *)(sp + 4 * k);
-                        const float4v bb = *(const float4v *)(args.bias + col0 + 4 * k);
+                        const float4v bb = *(const float4v *)(args.bias + n0 + c + 4 * k);
 #pragma unroll
-                        for (int j = 0; j < 4; j++) hv[4 * k + j] = args.gelu_tab[f2h(bb[j] + v[j])];  // gelu(b + W.x)
+                        for (int j = 0; j < 4; j++) y[4 * k + j] = h2f((uint16_t)half_table(gtab, args.gelu, f2h(bb[j] + v[j])));
                     }
-#pragma unroll
-                    for (int j = 0; j < 32; j++) y[j] = h2f(hv[j]);
-                    store_act_block<WT>(args.out_act, args.N, row0 + r, col0 >> 5, y);
+                    store_act_quarter<WT>(args.out_act, args.N, row0 + r, (n0 >> 5) + b, qq, y);
                 }
             } else {
-                ln_row_phase_t<WT, NBLK>(stage, LD, red, row0, args.bias, args.X, args.ln_w, args.ln_b, args.eps,
+                ln_row_phase_q<WT, NBLK>(stage, LD, red, row0, args.bias, args.X, args.ln_w, args.ln_b, args.eps,
                                          args.out_act, tid, NT);
             }
         }
@@ -646,211 +723,225 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
 }
 
 // ---------------------------------------------------------------------------
-// Attention for sentences of n <= 128 tokens: one workgroup per (head,
-// sentence), wave w owns queries 32w..32w+31 (reference bert.cpp:928-942).
+// Attention for sentences of n <= 128 tokens (reference bert.cpp:928-942):
+// one workgroup per (sentence, group of heads), wave w owns queries
+// 32w..32w+31; heads of the group are processed in turn, so ggml's exp table
+// is copied into LDS once per workgroup.
 //
-// f32 accuracy on fp16 MFMA: every operand x is split exactly into
-// hi = fp16(x), lo = fp16(x - hi) and a product is hi*hi + hi*lo + lo*hi
-// (three v_mfma_f32_32x32x16_f16; the dropped lo*lo term is 2^-22 relative),
-// so S and the context carry f32-level error like ggml's f32 mul_mat.
-// Swapped QK^T: S^T = K . Q^T puts one query per lane column, so ggml's
-// soft_max (max, p = exp_tab[fp16(s - max)], double sum, p *= (float)(1/sum))
-// runs in registers (one cross-half shuffle), and the normalised P^T
-// accumulator is directly the B operand of ctx^T = V^T . P^T (no LDS round trip
-// for P).  K (row-major) and V^T are staged once per workgroup in LDS as hi/lo
-// planes; the context is quantised to the O-projection's activation format in
-// registers.
+// f32 accuracy on fp16 MFMA: the QKV GEMM stored every value x split exactly
+// into hi = fp16(x), lo = fp16(x - hi); K.Q^T is hi*hi + hi*lo + lo*hi (three
+// v_mfma_f32_32x32x16_f16; the dropped lo*lo term is 2^-22 relative), so S
+// carries f32-level error like ggml's f32 mul_mat.  Swapped QK^T: S^T = K . Q^T
+// puts one query per lane column, so ggml's soft_max (max, p =
+// exp_tab[fp16(s - max)], double sum, scale by (float)(1/sum)) runs in
+// registers with one cross-half shuffle.  The probabilities are fp16 table
+// values, exact as MFMA operands: ctx^T = (V^T_hi + V^T_lo) . P^T in two MFMAs
+// with exact products and f32 accumulation, then the 1/sum scale is applied to
+// the 32 outputs of each query (ggml scales P first: the two orders differ by
+// f32 rounding only).  The context is quantised to the O-projection's
+// activation format in registers.
+
 template <int WT, int D>
-__global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int heads_per_wg) {
     constexpr int NK = 128;      // keys staged (n <= 128)
     constexpr int KST = D + 8;   // K row stride, halves: conflict-free ds_read_b128 (80 / 144 B)
     constexpr int VST = NK + 4;  // V^T row stride, halves: 66 dwords, conflict-free ds_read_b64
     __shared__ __attribute__((aligned(16))) _Float16 Kh[NK * KST], Kl[NK * KST], Vh[D * VST], Vl[D * VST];
-    const int h = blockIdx.x, s = blockIdx.y;
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
+    const int s = blockIdx.y;
     const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
     if (n > NK) return;  // attention_long_kernel handles these sentences
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
-    const int E = a.E, E3 = 3 * E;
-    const float *base = a.qkv + (int64_t)beg * E3;
+    const int E = a.E, E2 = 2 * E;
+    const bool v_aligned = (beg & 7) == 0;
+    const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
+    for (int i = tid; i < a.expt.n_pad / 8; i += 256) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
 
-    for (int idx = tid; idx < NK * (D / 4); idx += 256) {
-        const int key = idx / (D / 4), d0 = (idx - key * (D / 4)) * 4;
-        float4v k = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
-        if (key < n) {
-            k = *(const float4v *)(base + (int64_t)key * E3 + E + h * D + d0);
-            v = *(const float4v *)(base + (int64_t)key * E3 + 2 * E + h * D + d0);
-        }
-        half4v khi, klo;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            khi[j] = (_Float16)k[j];
-            klo[j] = (_Float16)(k[j] - (float)khi[j]);
-            const _Float16 vh = (_Float16)v[j];
-            Vh[(d0 + j) * VST + key] = vh;
-            Vl[(d0 + j) * VST + key] = (_Float16)(v[j] - (float)vh);
-        }
-        *(half4v *)&Kh[key * KST + d0] = khi;
-        *(half4v *)&Kl[key * KST + d0] = klo;
-    }
-    __syncthreads();
-    const int q0 = wv * 32;
-    if (q0 >= n) return;
-
-    // Q^T fragments (B operand): lane (r, hh) holds Q[q0 + r][16 ks + 8 hh + j]
-    half8 qh[D / 16], ql[D / 16];
-    {
-        const int qr = min(q0 + r, n - 1);
-        const float *qp = base + (int64_t)qr * E3 + h * D + 8 * hh;
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ks++) {
-            const float4v x0 = *(const float4v *)(qp + 16 * ks), x1 = *(const float4v *)(qp + 16 * ks + 4);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                qh[ks][j] = (_Float16)x0[j];
-                ql[ks][j] = (_Float16)(x0[j] - (float)qh[ks][j]);
-                qh[ks][4 + j] = (_Float16)x1[j];
-                ql[ks][4 + j] = (_Float16)(x1[j] - (float)qh[ks][4 + j]);
+    const int h_beg = blockIdx.x * heads_per_wg, h_end = min(h_beg + heads_per_wg, a.H);
+    for (int h = h_beg; h < h_end; h++) {
+        __syncthreads();  // previous head's LDS reads are done
+        for (int idx = tid; idx < NK * (D / 8); idx += 256) {
+            const int key = idx / (D / 8), c = (idx - key * (D / 8)) * 8;
+            uint4 kh = {0u, 0u, 0u, 0u}, kl = {0u, 0u, 0u, 0u};
+            if (key < n) {
+                const int64_t off = (int64_t)(beg + key) * E2 + E + h * D + c;
+                kh = *(const uint4 *)(a.qk_hi + off);
+                kl = *(const uint4 *)(a.qk_lo + off);
             }
+            *(uint4 *)&Kh[key * KST + c] = kh;
+            *(uint4 *)&Kl[key * KST + c] = kl;
         }
-    }
-    const int nkt = (n + 31) >> 5;
-    float16v S[4];
-    const float16v zero16 = {};
+        for (int idx = tid; idx < D * (NK / 8); idx += 256) {
+            const int d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+            const int64_t off = (int64_t)(h * D + d) * a.ldv + beg + k8;
+            half8 vh = {}, vl = {};
+            if (k8 + 8 <= n && v_aligned) {
+                vh = *(const half8 *)(a.vt_hi + off);
+                vl = *(const half8 *)(a.vt_lo + off);
+            } else {
 #pragma unroll
-    for (int kt = 0; kt < 4; kt++) {
-        S[kt] = zero16;
-        if (kt < nkt) {
+                for (int j = 0; j < 8; j++)
+                    if (k8 + j < n) {
+                        vh[j] = ((const _Float16 *)a.vt_hi)[off + j];
+                        vl[j] = ((const _Float16 *)a.vt_lo)[off + j];
+                    }
+            }
+            *(half4v *)&Vh[d * VST + k8] = half4v{vh[0], vh[1], vh[2], vh[3]};
+            *(half4v *)&Vh[d * VST + k8 + 4] = half4v{vh[4], vh[5], vh[6], vh[7]};
+            *(half4v *)&Vl[d * VST + k8] = half4v{vl[0], vl[1], vl[2], vl[3]};
+            *(half4v *)&Vl[d * VST + k8 + 4] = half4v{vl[4], vl[5], vl[6], vl[7]};
+        }
+        __syncthreads();
+        const int q0 = wv * 32;
+        if (q0 >= n) continue;
+
+        // Q^T fragments (B operand): lane (r, hh) holds Q[q0 + r][16 ks + 8 hh + j]
+        half8 qh[D / 16], ql[D / 16];
+        {
+            const int qr = min(q0 + r, n - 1);
+            const int64_t off = (int64_t)(beg + qr) * E2 + h * D + 8 * hh;
 #pragma unroll
             for (int ks = 0; ks < D / 16; ks++) {
-                const int off = (kt * 32 + r) * KST + 16 * ks + 8 * hh;
-                const half8 kh = *(const half8 *)&Kh[off], kl = *(const half8 *)&Kl[off];
-                S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], S[kt], 0, 0, 0);
-                S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], S[kt], 0, 0, 0);
-                S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], S[kt], 0, 0, 0);
+                qh[ks] = *(const half8 *)(a.qk_hi + off + 16 * ks);
+                ql[ks] = *(const half8 *)(a.qk_lo + off + 16 * ks);
             }
         }
-    }
-    // soft_max over keys for query q0 + r: this lane holds keys
-    // 32 kt + (j & 3) + 8 (j >> 2) + 4 hh, the partner lane (r, 1 - hh) the rest
-    float mx = -INFINITY;
+        const int nkt = (n + 31) >> 5;
+        float16v S[4];
+        const float16v zero16 = {};
 #pragma unroll
-    for (int kt = 0; kt < 4; kt++)
+        for (int kt = 0; kt < 4; kt++) {
+            S[kt] = zero16;
+            if (kt < nkt) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int key = kt * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh;
-            const float sv = key < n ? S[kt][j] * a.scale : -INFINITY;  // ggml_scale after K.Q
-            S[kt][j] = sv;
-            mx = fmaxf(mx, sv);
-        }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    double sum = 0.0;
-#pragma unroll
-    for (int kt = 0; kt < 4; kt++)
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const float p = h2f(a.exp_tab[f2h(S[kt][j] - mx)]);  // -inf -> table -> 0
-            S[kt][j] = p;
-            sum += (double)p;
-        }
-    sum += __shfl_xor(sum, 32);
-    const float rs = (float)(1.0 / sum);
-    // ctx^T = V^T . P^T.  k-step ks of key tile kt: B element j of lane half hh
-    // is key 32 kt + 16 ks + 8 (j >> 2) + 4 hh + (j & 3) = register 8 ks + j.
-    float16v o[D / 32];
-#pragma unroll
-    for (int dt = 0; dt < D / 32; dt++) o[dt] = zero16;
-#pragma unroll
-    for (int kt = 0; kt < 4; kt++) {
-        if (kt < nkt) {
-#pragma unroll
-            for (int ks = 0; ks < 2; ks++) {
-                half8 ph, pl;
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const float p = S[kt][8 * ks + j] * rs;  // ggml: p *= (float)(1/sum) before V.P
-                    ph[j] = (_Float16)p;
-                    pl[j] = (_Float16)(p - (float)ph[j]);
-                }
-                const int key = kt * 32 + 16 * ks + 4 * hh;
-#pragma unroll
-                for (int dt = 0; dt < D / 32; dt++) {
-                    const int off = (dt * 32 + r) * VST + key;
-                    const half4v h0 = *(const half4v *)&Vh[off], h1 = *(const half4v *)&Vh[off + 8];
-                    const half4v l0 = *(const half4v *)&Vl[off], l1 = *(const half4v *)&Vl[off + 8];
-                    const half8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-                    const half8 vl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o[dt], 0, 0, 0);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[dt], 0, 0, 0);
+                for (int ks = 0; ks < D / 16; ks++) {
+                    const int off = (kt * 32 + r) * KST + 16 * ks + 8 * hh;
+                    const half8 kh = *(const half8 *)&Kh[off], kl = *(const half8 *)&Kl[off];
+                    S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], S[kt], 0, 0, 0);
+                    S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], S[kt], 0, 0, 0);
+                    S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], S[kt], 0, 0, 0);
                 }
             }
         }
-    }
-    // lane (r, hh) holds ctx[q0 + r][h D + 32 dt + (j & 3) + 8 (j >> 2) + 4 hh]:
-    // one 32-value quant block per (query, dt), split over the lane pair (r, hh).
-    const int q = q0 + r;
-    const int64_t row = beg + q;
+        // soft_max over keys for query q0 + r: this lane holds keys
+        // 32 kt + (j & 3) + 8 (j >> 2) + 4 hh, the partner lane (r, 1 - hh) the rest
+        float mx = -INFINITY;
 #pragma unroll
-    for (int dt = 0; dt < D / 32; dt++) {
-        const int col0 = h * D + dt * 32;
-        if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
-            float amax = 0.f;
+        for (int kt = 0; kt < 4; kt++) {
+            if (kt < nkt) {
+                const bool partial = 32 * kt + 32 > n;
 #pragma unroll
-            for (int j = 0; j < 16; j++) amax = fmaxf(amax, fabsf(o[dt][j]));
-            amax = fmaxf(amax, __shfl_xor(amax, 32));
-            const float d = amax / 127.f;
-            const float id = amax != 0.f ? 127.f / amax : 0.f;
-            int qs = 0;
-            uint32_t pk[4];
-#pragma unroll
-            for (int m = 0; m < 4; m++) {
-                uint32_t x = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int qv = (int)rintf(o[dt][4 * m + j] * id);
-                    qs += qv;
-                    x |= ((uint32_t)(qv & 0xff)) << (8 * j);
+                for (int j = 0; j < 16; j++) {
+                    float sv = S[kt][j] * a.scale;  // ggml_scale after K.Q
+                    if (partial && 32 * kt + (j & 3) + 8 * (j >> 2) + 4 * hh >= n) sv = -INFINITY;
+                    S[kt][j] = sv;
+                    mx = fmaxf(mx, sv);
                 }
-                pk[m] = x;
             }
-            qs += __shfl_xor(qs, 32);
-            if (q < n) {
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        double sum = 0.0;
 #pragma unroll
-                for (int m = 0; m < 4; m++) *(uint32_t *)((int8_t *)a.ctx.q + row * E + col0 + 8 * m + 4 * hh) = pk[m];
-                if (hh == 0) {
-                    const int64_t bi = row * (E >> 5) + (col0 >> 5);
-                    if constexpr (WT == W_Q4_0) {
-                        ((uint16_t *)a.ctx.d)[bi] = f2h(d);
-                    } else {
-                        ((float *)a.ctx.d)[bi] = d;
-                        ((float *)a.ctx.s)[bi] = d * (float)qs;
+        for (int kt = 0; kt < 4; kt++) {
+            if (kt < nkt) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    // s - max <= 0: exp_tab[fp16(s - max)] from LDS; -inf (masked) -> 0
+                    const uint32_t hm = f2h(S[kt][j] - mx) & 0x7fffu;
+                    const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
+                    S[kt][j] = p;
+                    sum += (double)p;
+                }
+            }
+        }
+        sum += __shfl_xor(sum, 32);
+        const float rs = (float)(1.0 / sum);
+        // ctx^T = V^T . P^T.  k-step ks of key tile kt: B element j of lane half hh
+        // is key 32 kt + 16 ks + 8 (j >> 2) + 4 hh + (j & 3) = register 8 ks + j.
+        float16v o[D / 32];
+#pragma unroll
+        for (int dt = 0; dt < D / 32; dt++) o[dt] = zero16;
+#pragma unroll
+        for (int kt = 0; kt < 4; kt++) {
+            if (kt < nkt) {
+#pragma unroll
+                for (int ks = 0; ks < 2; ks++) {
+                    half8 ph;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) ph[j] = (_Float16)S[kt][8 * ks + j];  // exact: fp16 table values
+                    const int key = kt * 32 + 16 * ks + 4 * hh;
+#pragma unroll
+                    for (int dt = 0; dt < D / 32; dt++) {
+                        const int off = (dt * 32 + r) * VST + key;
+                        const half4v h0 = *(const half4v *)&Vh[off], h1 = *(const half4v *)&Vh[off + 8];
+                        const half4v l0 = *(const half4v *)&Vl[off], l1 = *(const half4v *)&Vl[off + 8];
+                        const half8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+                        const half8 vl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[dt], 0, 0, 0);
                     }
                 }
             }
-        } else if (q < n) {
+        }
+        // lane (r, hh) holds ctx[q0 + r][h D + 32 dt + (j & 3) + 8 (j >> 2) + 4 hh]:
+        // one 32-value quant block per (query, dt), split over the lane pair (r, hh).
+        const int q = q0 + r;
+        const int64_t row = beg + q;
 #pragma unroll
-            for (int m = 0; m < 4; m++) {
-                const int col = col0 + 8 * m + 4 * hh;
-                if constexpr (WT == W_F16) {
-                    *(half4v *)((_Float16 *)a.ctx.q + row * E + col) =
-                        half4v{(_Float16)o[dt][4 * m], (_Float16)o[dt][4 * m + 1], (_Float16)o[dt][4 * m + 2],
-                               (_Float16)o[dt][4 * m + 3]};
-                } else {
-                    *(float4v *)((float *)a.ctx.q + row * E + col) =
-                        float4v{o[dt][4 * m], o[dt][4 * m + 1], o[dt][4 * m + 2], o[dt][4 * m + 3]};
+        for (int dt = 0; dt < D / 32; dt++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) o[dt][j] *= rs;
+            const int col0 = h * D + dt * 32;
+            if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+                float amax = 0.f;
+#pragma unroll
+                for (int j = 0; j < 16; j++) amax = fmaxf(amax, fabsf(o[dt][j]));
+                amax = fmaxf(amax, __shfl_xor(amax, 32));
+                const float d = amax / 127.f;
+                const float id = amax != 0.f ? 127.f / amax : 0.f;
+                uint32_t pk[4];
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int qv = (int)rintf(o[dt][4 * m + j] * id);
+                        x |= ((uint32_t)(qv & 0xff)) << (8 * j);
+                    }
+                    pk[m] = x;
+                }
+                if (q < n) {
+#pragma unroll
+                    for (int m = 0; m < 4; m++) *(uint32_t *)((int8_t *)a.ctx.q + row * E + col0 + 8 * m + 4 * hh) = pk[m];
+                    if (hh == 0) {
+                        const int64_t bi = row * (E >> 5) + (col0 >> 5);
+                        if constexpr (WT == W_Q4_0) {
+                            ((uint16_t *)a.ctx.d)[bi] = f2h(d);
+                        } else {
+                            ((float *)a.ctx.d)[bi] = d;
+                        }
+                    }
+                }
+            } else if (q < n) {
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    const int col = col0 + 8 * m + 4 * hh;
+                    if constexpr (WT == W_F16) {
+                        *(half4v *)((_Float16 *)a.ctx.q + row * E + col) =
+                            half4v{(_Float16)o[dt][4 * m], (_Float16)o[dt][4 * m + 1], (_Float16)o[dt][4 * m + 2],
+                                   (_Float16)o[dt][4 * m + 3]};
+                    } else {
+                        *(float4v *)((float *)a.ctx.q + row * E + col) =
+                            float4v{o[dt][4 * m], o[dt][4 * m + 1], o[dt][4 * m + 2], o[dt][4 * m + 3]};
+                    }
                 }
             }
         }
     }
 }
 
-// ---------------------------------------------------------------------------
-// Attention for sentences of n > 128 tokens, one (sentence, head, 64-query block)
-// per workgroup: 4 waves x 16 queries.
-// S = (K.Q) * scale on f32 MFMA (exact f32 products, as ggml's f32 mul_mat),
-// rows kept in LDS; ggml_soft_max: max, p = exp_tab[fp16(s - max)], double
-// sum, p *= (float)(1/sum); ctx = V^T.P on f32 MFMA; quantised to the O-proj's
-// activation format in the epilogue.
+// Attention for 128 < n <= 512 (f32 MFMA on the reconstructed hi + lo values;
+// scores through LDS).  One workgroup per (64 queries, head, sentence).
 template <int WT, int D>
 __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
@@ -858,25 +949,29 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
     const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
     if (q0 >= n || n <= 128) return;  // n <= 128: attention_short_kernel
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4, c16 = lane & 15;
-    const int E = a.E, E3 = 3 * E;
+    const int E = a.E, E2 = 2 * E;
     const int nk16 = (n + 15) & ~15;
     const int LDS_S = ((nk16 + 55) / 64) * 64 + 8;  // == 8 (mod 64) dwords: conflict-free float4 row reads
     float *S = (float *)dsm + wv * 16 * LDS_S;
-    const float *base = a.qkv + (int64_t)beg * E3;
     const int qw0 = q0 + wv * 16;  // this wave's first query
 
+    auto ld4 = [&](int64_t off) {  // hi + lo of four consecutive Q|K values
+        const half4v hv = *(const half4v *)((const _Float16 *)a.qk_hi + off), lv = *(const half4v *)((const _Float16 *)a.qk_lo + off);
+        return float4v{(float)hv[0] + (float)lv[0], (float)hv[1] + (float)lv[1], (float)hv[2] + (float)lv[2],
+                       (float)hv[3] + (float)lv[3]};
+    };
     float4v qf[D / 16];
     {
         const int qr = min(qw0 + c16, n - 1);
 #pragma unroll
-        for (int c = 0; c < D / 16; c++) qf[c] = *(const float4v *)(base + (int64_t)qr * E3 + h * D + 16 * c + 4 * g);
+        for (int c = 0; c < D / 16; c++) qf[c] = ld4((int64_t)(beg + qr) * E2 + h * D + 16 * c + 4 * g);
     }
     for (int key0 = 0; key0 < n; key0 += 16) {
         const int kr = min(key0 + c16, n - 1);
         float4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < D / 16; c++) {
-            const float4v kf = *(const float4v *)(base + (int64_t)kr * E3 + E + h * D + 16 * c + 4 * g);
+            const float4v kf = ld4((int64_t)(beg + kr) * E2 + E + h * D + 16 * c + 4 * g);
 #pragma unroll
             for (int j = 0; j < 4; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[c][j], kf[j], acc, 0, 0, 0);
         }
@@ -893,7 +988,7 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
         mx = fmaxf(mx, __shfl_xor(mx, 2));
         double sum = 0.0;
         for (int k = part; k < n; k += 4) {
-            const float p = h2f(a.exp_tab[f2h(row[k] - mx)]);
+            const float p = h2f(a.expt.full[f2h(row[k] - mx)]);
             row[k] = p;
             sum += (double)p;
         }
@@ -907,7 +1002,6 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
     float4v o[D / 16];
 #pragma unroll
     for (int dt = 0; dt < D / 16; dt++) o[dt] = float4v{0.f, 0.f, 0.f, 0.f};
-    const float *vbase = base + 2 * E + h * D;
     for (int kc = 0; kc < nk16; kc += 16) {
         const float4v pf = *(const float4v *)(S + c16 * LDS_S + kc + 4 * g);
 #pragma unroll
@@ -915,7 +1009,8 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
             const int vr = min(kc + 4 * g + j, n - 1);
 #pragma unroll
             for (int dt = 0; dt < D / 16; dt++) {
-                const float vv = vbase[(int64_t)vr * E3 + dt * 16 + c16];
+                const int64_t vo = (int64_t)(h * D + dt * 16 + c16) * a.ldv + beg + vr;
+                const float vv = h2f(a.vt_hi[vo]) + h2f(a.vt_lo[vo]);
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[j], vv, o[dt], 0, 0, 0);
             }
         }
@@ -996,24 +1091,35 @@ static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Wave tiles hold 4 n-tiles (64 columns) for QKV / FFN-up (64-row tiles); the
-// LayerNorm GEMMs own whole rows (BN = E) and use 32-row tiles to keep the
-// row-statistics epilogue inside the register budget.
+// Q4 weights (split hi/lo planes, two MFMAs per block): waves own 32 columns x
+// 128 rows, so each W fragment pair read from L2 feeds 8 row tiles and the
+// L2 stream stays at (M/128) * N * K * 4 bytes.  F16/F32: waves own 64 columns x
+// 64 rows.  LayerNorm GEMMs own whole rows (BN = E).
 template <int WT>
 static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
-    if (epi == EPI_BIAS_F32) return gemm_t<WT, EPI_BIAS_F32, 384, 6, 64>(a, Mpad, s);
-    if (epi == EPI_GELU_ACT) return gemm_t<WT, EPI_GELU_ACT, 256, 4, 64>(a, Mpad, s);
-    switch (a.N) {
-        case 384: return gemm_t<WT, EPI_LN, 384, 6, 64>(a, Mpad, s);
-        case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);
-        case 1024: return gemm_t<WT, EPI_LN, 1024, 8, 32>(a, Mpad, s);
+    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+        if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
+        if (epi == EPI_GELU_ACT) return gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
+        switch (a.N) {
+            case 384: return gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
+            case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);
+            case 1024: return gemm_t<WT, EPI_LN, 1024, 16, 32>(a, Mpad, s);
+        }
+    } else {
+        if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 6, 64>(a, Mpad, s);
+        if (epi == EPI_GELU_ACT) return gemm_t<WT, EPI_GELU_ACT, 256, 4, 64>(a, Mpad, s);
+        switch (a.N) {
+            case 384: return gemm_t<WT, EPI_LN, 384, 6, 64>(a, Mpad, s);
+            case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);
+            case 1024: return gemm_t<WT, EPI_LN, 1024, 8, 32>(a, Mpad, s);
+        }
     }
     return hipErrorInvalidValue;
 }
 
 bool gemm_shape_supported(int epi, int N, int K) {
     if (K % KC) return false;
-    if (epi == EPI_BIAS_F32) return N % 384 == 0;
+    if (epi == EPI_QKV) return N % 384 == 0;
     if (epi == EPI_GELU_ACT) return N % 256 == 0;
     return N == 384 || N == 768 || N == 1024;
 }
@@ -1031,7 +1137,11 @@ hipError_t launch_gemm(int wtype, int epi, int /*unused*/, const GemmArgs &a, in
 
 template <int WT, int D>
 static hipError_t attn_t(const AttnArgs &a, int n_seqs, int max_len, hipStream_t s) {
-    hipLaunchKernelGGL((attention_short_kernel<WT, D>), dim3(a.H, n_seqs), dim3(256), 0, s, a);
+    // heads per workgroup: all of a sentence's heads when the batch alone fills
+    // the GPU (the exp table is staged once), fewer for small batches
+    const int hpw = std::max(1, std::min(a.H, n_seqs / 64));
+    const int groups = (a.H + hpw - 1) / hpw;
+    hipLaunchKernelGGL((attention_short_kernel<WT, D>), dim3(groups, n_seqs), dim3(256), 0, s, a, hpw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || max_len <= 128) return e;
     const int nk16 = (max_len + 15) & ~15;

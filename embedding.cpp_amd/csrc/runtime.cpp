@@ -62,8 +62,48 @@ void set_err(const char *fmt, ...) {
 
 // ggml_init's fp16 tables (GELU tanh form and exp), built with this host's libm
 // exactly like ggml builds them.
+// Compact LDS view of a full table (kernels.h HalfTable): the shortest
+// [0, pos_n) / [0x8000, 0x8000 + neg_n) ranges outside which every finite
+// entry is h itself (positive side, if allowed) or one constant (negative side).
+struct CompactTable {
+    std::vector<uint16_t> compact;
+    int pos_n = 0, neg_n = 0, pos_identity = 0;
+    uint32_t neg_const = 0;
+};
+CompactTable compact_table(const std::vector<uint16_t> &full, bool identity_tail, int pos_n_fixed) {
+    CompactTable c;
+    if (identity_tail) {
+        int p = 0x7c00;
+        while (p > 0 && full[(size_t)(p - 1)] == (uint16_t)(p - 1)) p--;
+        c.pos_n = p;
+        c.pos_identity = 1;
+    } else {
+        c.pos_n = pos_n_fixed;  // positives beyond it read the global table
+    }
+    c.neg_const = full[0xfbff];
+    int n = 0x7c00;
+    while (n > 0 && full[(size_t)(0x8000 | (n - 1))] == c.neg_const) n--;
+    c.neg_n = n;
+    const int tot = c.pos_n + c.neg_n + 1, pad = (tot + 7) / 8 * 8;  // + neg_const at [pos_n + neg_n]
+    c.compact.assign((size_t)pad, 0);
+    c.compact[(size_t)(c.pos_n + c.neg_n)] = (uint16_t)c.neg_const;
+    for (int h = 0; h < c.pos_n; h++) c.compact[(size_t)h] = full[(size_t)h];
+    for (int m = 0; m < c.neg_n; m++) c.compact[(size_t)(c.pos_n + m)] = full[(size_t)(0x8000 | m)];
+    // self-check: the device lookup rule (kernels.hip half_table) reproduces every entry
+    for (uint32_t h = 0; h < 65536; h++) {
+        const uint32_t mag = h & 0x7fffu;
+        const bool neg = (h & 0x8000u) != 0;
+        const bool in = neg ? mag < (uint32_t)c.neg_n : mag < (uint32_t)c.pos_n;
+        if (mag >= 0x7c00u || (!neg && !in && !c.pos_identity)) continue;  // read from the full table
+        const uint32_t v = in ? c.compact[neg ? c.pos_n + mag : mag] : (neg ? c.neg_const : h);
+        if (v != full[h]) c.pos_n = c.neg_n = 1 << 20;  // poison: load_impl reports it
+    }
+    return c;
+}
+
 struct HostTables {
     std::vector<uint16_t> gelu, expt;
+    CompactTable gelu_c, exp_c;
     HostTables() : gelu(65536), expt(65536) {
         const float A = 0.044715f, S = 0.79788456080286535587989211986876f;
         for (int i = 0; i < 65536; i++) {
@@ -72,10 +112,23 @@ struct HostTables {
             gelu[i] = f32_to_f16(g);
             expt[i] = f32_to_f16(expf(f));
         }
+        gelu_c = compact_table(gelu, true, 0);
+        exp_c = compact_table(expt, false, 1);  // soft_max only feeds s - max <= 0
     }
 };
 const HostTables &tables() {
     static HostTables t;
+    return t;
+}
+HalfTable half_table(const uint16_t *full, const uint16_t *compact, const CompactTable &c) {
+    HalfTable t;
+    t.full = full;
+    t.compact = compact;
+    t.pos_n = c.pos_n;
+    t.neg_n = c.neg_n;
+    t.n_pad = (int)c.compact.size();
+    t.pos_identity = c.pos_identity;
+    t.neg_const = c.neg_const;
     return t;
 }
 
@@ -97,7 +150,8 @@ struct DevLayer {
 struct Workspace {
     int64_t cap_rows = 0;   // padded rows
     int64_t cap_seqs = 0;
-    float *X = nullptr, *QKV = nullptr, *out = nullptr;
+    float *X = nullptr, *out = nullptr;
+    uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16: kernels.h GemmArgs EPI_QKV
     ActPtr Xa, Ca, Ua;
     int32_t *tok = nullptr, *off = nullptr;
     std::vector<void *> allocs;
@@ -118,7 +172,7 @@ struct Replica {
     void *word = nullptr, *pos = nullptr, *type = nullptr;
     float *ln_e_w = nullptr, *ln_e_b = nullptr;
     std::vector<DevLayer> L;
-    uint16_t *gelu_tab = nullptr, *exp_tab = nullptr;
+    uint16_t *gelu_tab = nullptr, *exp_tab = nullptr, *gelu_compact = nullptr, *exp_compact = nullptr;
     std::vector<void *> weight_allocs;
     Workspace ws;
     // profiling: events recorded around each launch when enabled
@@ -171,7 +225,8 @@ bool upload(std::vector<void *> &track, T **p, const void *src, size_t bytes) {
 // Repack a [N][K] ggml-format matrix (given as row pointers) into MFMA
 // fragment order (kernels.h WPtr).
 struct Packed {
-    std::vector<uint8_t> q, d, m;
+    std::vector<uint8_t> q;
+    float unscale = 1.f;
 };
 
 Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_t K) {
@@ -184,32 +239,54 @@ Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_
             for (int c = 0; c < 16; c++) rows[(size_t)(32 * pr + 16 * t + c)] = rows_in[(size_t)(32 * pr + 2 * c + t)];
     Packed p;
     if (type == GT_Q4_0 || type == GT_Q4_1) {
+        // w = d*(q-8) | d*q + m, exact in double; scaled by 2^S so that
+        // max|w| lands in [2^13, 2^14): the fp16 hi part stays far from
+        // overflow and the lo part stays normal for all but negligible weights
         const int bs = type == GT_Q4_0 ? 18 : 20, qoff = type == GT_Q4_0 ? 2 : 4;
-        p.q.resize((size_t)ntl * nkb * 64 * 4);
-        p.d.resize((size_t)ntl * nkb * 16 * 2);
-        if (type == GT_Q4_1) p.m.resize(p.d.size());
-        uint32_t *q = (uint32_t *)p.q.data();
-        uint16_t *d = (uint16_t *)p.d.data(), *m = (uint16_t *)p.m.data();
-        for (int64_t nt = 0; nt < ntl; nt++)
+        auto wval = [&](const uint8_t *row, int64_t k) -> double {
+            const uint8_t *blk = row + (k >> 5) * bs;
+            const int e = (int)(k & 31);
+            const uint8_t byte = blk[qoff + (e & 15)];
+            const int qv = e < 16 ? (byte & 15) : (byte >> 4);
+            uint16_t dh, mh;
+            std::memcpy(&dh, blk, 2);
+            const double d = f16_to_f32(dh);
+            if (type == GT_Q4_0) return d * (qv - 8);
+            std::memcpy(&mh, blk + 2, 2);
+            return d * qv + (double)f16_to_f32(mh);
+        };
+        double amax = 0.0;
+        for (int64_t n = 0; n < N; n++)
             for (int64_t kb = 0; kb < nkb; kb++) {
-                const int64_t t = nt * nkb + kb;
+                const uint8_t *blk = rows[(size_t)n] + kb * bs;
+                uint16_t dh, mh = 0;
+                std::memcpy(&dh, blk, 2);
+                if (type == GT_Q4_1) std::memcpy(&mh, blk + 2, 2);
+                const double d = std::fabs((double)f16_to_f32(dh)), m = (double)f16_to_f32(mh);
+                amax = std::max(amax, type == GT_Q4_0 ? 8.0 * d : std::max(std::fabs(m), std::fabs(m + 15.0 * d)));
+            }
+        int S = 0;
+        if (amax > 0.0) {
+            int e2;
+            std::frexp(amax, &e2);  // amax in [2^(e2-1), 2^e2)
+            S = 14 - e2;
+        }
+        const double scale = std::ldexp(1.0, S);
+        p.unscale = (float)std::ldexp(1.0, -S);
+        p.q.resize((size_t)N * K * 4);
+        uint16_t *q = (uint16_t *)p.q.data();
+        for (int64_t nt = 0; nt < ntl; nt++)
+            for (int64_t kb = 0; kb < nkb; kb++)
                 for (int lane = 0; lane < 64; lane++) {
                     const int c = lane & 15, g = lane >> 4;
-                    const uint8_t *blk = rows[nt * 16 + c] + kb * bs;
-                    uint32_t x = 0;
-                    for (int s = 0; s < 8; s++) {
-                        const int e = 8 * g + (s < 4 ? 2 * s : 2 * (s - 4) + 1);
-                        const uint8_t byte = blk[qoff + (e & 15)];
-                        const uint32_t qv = e < 16 ? (byte & 15u) : (byte >> 4);
-                        x |= qv << (4 * s);
-                    }
-                    q[t * 64 + lane] = x;
-                    if (g == 0) {
-                        std::memcpy(&d[t * 16 + c], blk, 2);
-                        if (type == GT_Q4_1) std::memcpy(&m[t * 16 + c], blk + 2, 2);
+                    uint16_t *hi = &q[(((nt * nkb + kb) * 2 + 0) * 64 + lane) * 8];
+                    uint16_t *lo = &q[(((nt * nkb + kb) * 2 + 1) * 64 + lane) * 8];
+                    for (int j = 0; j < 8; j++) {
+                        const double w = wval(rows[(size_t)(nt * 16 + c)], kb * 32 + 8 * g + j) * scale;
+                        hi[j] = f32_to_f16((float)w);
+                        lo[j] = f32_to_f16((float)(w - (double)f16_to_f32(hi[j])));
                     }
                 }
-            }
     } else if (type == GT_F16) {
         p.q.resize((size_t)N * K * 2);
         uint16_t *q = (uint16_t *)p.q.data();
@@ -237,13 +314,10 @@ Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_
 }
 
 bool upload_packed(std::vector<void *> &track, WPtr &w, const Packed &p) {
-    void *q = nullptr, *d = nullptr, *m = nullptr;
+    void *q = nullptr;
     if (!upload(track, &q, p.q.data(), p.q.size())) return false;
-    if (!p.d.empty() && !upload(track, &d, p.d.data(), p.d.size())) return false;
-    if (!p.m.empty() && !upload(track, &m, p.m.data(), p.m.size())) return false;
     w.q = q;
-    w.d = d;
-    w.m = m;
+    w.unscale = p.unscale;
     return true;
 }
 
@@ -261,7 +335,6 @@ bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, i
     if (!dmalloc(track, &a.q, (size_t)rows * K * act_elem_bytes(wtype))) return false;
     if (act_scale_bytes(wtype) && !dmalloc(track, &a.d, (size_t)rows * (K / 32) * act_scale_bytes(wtype)))
         return false;
-    if (wtype == W_Q4_1 && !dmalloc(track, &a.s, (size_t)rows * (K / 32) * 4)) return false;
     return true;
 }
 
@@ -274,14 +347,19 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs) {
     const int64_t rows = std::max<int64_t>(Mpad, w.cap_rows), seqs = std::max<int64_t>(n_seqs, w.cap_seqs);
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const int wt = ctx->wtype;
-    if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.QKV, (size_t)rows * 3 * E * 4) ||
+    if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
+        !dmalloc(w.allocs, &w.qk_lo, (size_t)rows * 2 * E * 2) || !dmalloc(w.allocs, &w.vt_hi, (size_t)rows * E * 2) ||
+        !dmalloc(w.allocs, &w.vt_lo, (size_t)rows * E * 2) ||
         !alloc_act(w.allocs, w.Xa, wt, rows, E) || !alloc_act(w.allocs, w.Ca, wt, rows, E) ||
         !alloc_act(w.allocs, w.Ua, wt, rows, I) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
         !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4))
         return false;
     // padding rows must hold finite values: zero everything once
     HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, R.stream));
-    HIP_OK(hipMemsetAsync(w.QKV, 0, (size_t)rows * 3 * E * 4, R.stream));
+    HIP_OK(hipMemsetAsync(w.qk_hi, 0, (size_t)rows * 2 * E * 2, R.stream));
+    HIP_OK(hipMemsetAsync(w.qk_lo, 0, (size_t)rows * 2 * E * 2, R.stream));
+    HIP_OK(hipMemsetAsync(w.vt_hi, 0, (size_t)rows * E * 2, R.stream));
+    HIP_OK(hipMemsetAsync(w.vt_lo, 0, (size_t)rows * E * 2, R.stream));
     w.cap_rows = rows;
     w.cap_seqs = seqs;
     return true;
@@ -373,16 +451,24 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         q.W = L.qkv;
         q.N = 3 * E;
         q.bias = L.b_qkv;
-        q.out_f32 = w.QKV;
-        LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_BIAS_F32, 0, q, (int)Mpad, st));
+        q.qk_hi = w.qk_hi;
+        q.qk_lo = w.qk_lo;
+        q.vt_hi = w.vt_hi;
+        q.vt_lo = w.vt_lo;
+        q.ldv = w.cap_rows;
+        LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)Mpad, st));
 
         AttnArgs aa;
-        aa.qkv = w.QKV;
+        aa.qk_hi = w.qk_hi;
+        aa.qk_lo = w.qk_lo;
+        aa.vt_hi = w.vt_hi;
+        aa.vt_lo = w.vt_lo;
+        aa.ldv = w.cap_rows;
         aa.offsets = d_off;
         aa.E = E;
         aa.H = H;
         aa.scale = 1.0f / sqrtf((float)D);
-        aa.exp_tab = R.exp_tab;
+        aa.expt = half_table(R.exp_tab, R.exp_compact, tables().exp_c);
         aa.ctx = w.Ca;
         LAUNCH_OK("attention", launch_attention(wt, D, aa, n_seqs, max_len, st));
 
@@ -406,7 +492,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         u.N = I;
         u.bias = L.b_up;
         u.out_act = w.Ua;
-        u.gelu_tab = R.gelu_tab;
+        u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
         LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)Mpad, st));
 
         GemmArgs dn;
@@ -474,7 +560,9 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
         !upload(tr, &R.ln_e_w, hm.ln_e_w->data, hm.ln_e_w->nbytes) ||
         !upload(tr, &R.ln_e_b, hm.ln_e_b->data, hm.ln_e_b->nbytes) ||
         !upload(tr, &R.gelu_tab, tables().gelu.data(), 65536 * 2) ||
-        !upload(tr, &R.exp_tab, tables().expt.data(), 65536 * 2))
+        !upload(tr, &R.exp_tab, tables().expt.data(), 65536 * 2) ||
+        !upload(tr, &R.gelu_compact, tables().gelu_c.compact.data(), tables().gelu_c.compact.size() * 2) ||
+        !upload(tr, &R.exp_compact, tables().exp_c.compact.data(), tables().exp_c.compact.size() * 2))
         return false;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const uint32_t wt = hm.layers[0].q_w->type;
@@ -633,9 +721,14 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     ctx->type_t = hm.type->type;
     const int D = (int)(E / hp.n_head);
     if ((E != 384 && E != 768 && E != 1024) || (D != 32 && D != 64) || I % 256 || hp.n_max_tokens > 512 ||
-        !gemm_shape_supported(EPI_BIAS_F32, (int)(3 * E), (int)E) || !gemm_shape_supported(EPI_LN, (int)E, (int)I)) {
+        !gemm_shape_supported(EPI_QKV, (int)(3 * E), (int)E) || !gemm_shape_supported(EPI_LN, (int)E, (int)I)) {
         set_err("unsupported shape: n_embd=%d n_head=%d n_intermediate=%d n_max_tokens=%d", hp.n_embd, hp.n_head,
                 hp.n_intermediate, hp.n_max_tokens);
+        return nullptr;
+    }
+    if ((int)tables().gelu_c.compact.size() > HALF_TABLE_LDS || (int)tables().exp_c.compact.size() > EXP_TABLE_LDS) {
+        set_err("this host's libm gives fp16 GELU/exp tables whose compact part exceeds LDS (%zu, %zu entries)",
+                tables().gelu_c.compact.size(), tables().exp_c.compact.size());
         return nullptr;
     }
     // devices
