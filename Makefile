@@ -13,7 +13,7 @@ HOST_OBJS := $(addprefix $(BUILD)/obj/,$(HOST_SRCS:.cpp=.o))
 HIP_OBJS := $(BUILD)/obj/kernels.o
 CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
-HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
+HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
 
 all: $(BUILD)/libbert.so
 

@@ -133,70 +133,6 @@ __device__ __forceinline__ uint32_t half_table(const uint16_t *lds, const HalfTa
 }
 
 // ---------------------------------------------------------------------------
-// LayerNorm over 16 staged rows (ggml_norm + mul(repeat(w)) + add(repeat(b)),
-// reference bert.cpp:891-897/955-961/985-991): one thread per 32-column block,
-// double partial sums combined in a fixed order, two-pass mean/variance.
-// Optionally first adds bias and residual: v = (bias + acc) + resid.
-template <int WT, bool HAS_BIAS, bool HAS_RESID>
-__device__ void ln_row_phase(float *stage, int ld, int ncols, double *red, int64_t row0, const float *__restrict__ bias,
-                             float *X, const float *__restrict__ lnw, const float *__restrict__ lnb, float eps,
-                             const ActPtr &out, int tid, int nthreads) {
-    const int nblk = ncols >> 5, ntask = 16 * nblk;
-    double *red1 = red, *red2 = red + ntask;
-    for (int t = tid; t < ntask; t += nthreads) {
-        const int r = t / nblk, b = t - r * nblk;
-        float *sp = stage + r * ld + b * 32;
-        const float *xr = X + (row0 + r) * (int64_t)ncols + b * 32;
-        double s = 0.0;
-#pragma unroll 8
-        for (int j = 0; j < 32; j++) {
-            float v = sp[j];
-            if constexpr (HAS_BIAS) v = bias[b * 32 + j] + v;
-            if constexpr (HAS_RESID) v = v + xr[j];
-            sp[j] = v;
-            s += (double)v;
-        }
-        red1[t] = s;
-    }
-    __syncthreads();
-    for (int t = tid; t < ntask; t += nthreads) {
-        const int r = t / nblk, b = t - r * nblk;
-        double tot = 0.0;
-        for (int k = 0; k < nblk; k++) tot += red1[r * nblk + k];
-        const float mean = (float)(tot / ncols);
-        float *sp = stage + r * ld + b * 32;
-        double s2 = 0.0;
-#pragma unroll 8
-        for (int j = 0; j < 32; j++) {
-            const float v = sp[j] - mean;
-            sp[j] = v;
-            s2 += (double)(v * v);
-        }
-        red2[t] = s2;
-    }
-    __syncthreads();
-    for (int t = tid; t < ntask; t += nthreads) {
-        const int r = t / nblk, b = t - r * nblk;
-        double tot = 0.0;
-        for (int k = 0; k < nblk; k++) tot += red2[r * nblk + k];
-        const float var = (float)(tot / ncols);
-        const float scale = 1.0f / sqrtf(var + eps);
-        const float *sp = stage + r * ld + b * 32;
-        float y[32];
-#pragma unroll
-        for (int j = 0; j < 32; j++) {
-            float v = sp[j] * scale;
-            v = lnw[b * 32 + j] * v;
-            y[j] = v + lnb[b * 32 + j];
-        }
-        float4v *xo = (float4v *)(X + (row0 + r) * (int64_t)ncols + b * 32);
-#pragma unroll
-        for (int w = 0; w < 8; w++) xo[w] = float4v{y[4 * w], y[4 * w + 1], y[4 * w + 2], y[4 * w + 3]};
-        store_act_block<WT>(out, ncols, row0 + r, b, y);
-    }
-    __syncthreads();
-}
-
 // LayerNorm row phase for GEMM slices, four lanes per (row, 32-column block):
 // task t -> quarter qq = t & 3, block b, row r.  v = (bias + acc) + x; two-pass
 // statistics in double (ggml_norm), combined quarter -> block (two shuffles)
@@ -283,36 +219,50 @@ __device__ void ln_row_phase_q(float *stage, int ld, double *red, int64_t row0, 
 
 // ---------------------------------------------------------------------------
 // Embeddings: x = pos[i] + (type[0] + word[id]) then LayerNorm (bert.cpp:880-898).
-__device__ __forceinline__ float table_elem(const void *tab, int type, int64_t row, int E, int e) {
-    switch (type) {
-        case W_F32: return ((const float *)tab)[row * E + e];
-        case W_F16: return h2f(((const uint16_t *)tab)[row * E + e]);
-        case W_Q4_0: {
-            const uint8_t *blk = (const uint8_t *)tab + (row * (E >> 5) + (e >> 5)) * 18;
-            const uint16_t dh = (uint16_t)(blk[0] | (blk[1] << 8));
-            const int i = e & 31;
-            const uint8_t byte = blk[2 + (i & 15)];
-            const int q = i < 16 ? (byte & 15) : (byte >> 4);
-            return (float)(q - 8) * h2f(dh);
+// Eight consecutive elements e0..e0+7 (e0 % 8 == 0) of row `row` of a ggml
+// table (get_rows dequantisation: Q4_0 (q-8)*d, Q4_1 fmaf(q, d, m) as gcc
+// contracts ggml's x*d + m).
+__device__ __forceinline__ void table8(const void *tab, int type, int64_t row, int E, int e0, float *v) {
+    if (type == W_F32) {
+        const float4v *p = (const float4v *)((const float *)tab + row * E + e0);
+        const float4v x0 = p[0], x1 = p[1];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[j] = x0[j];
+            v[4 + j] = x1[j];
         }
-        default: {
-            const uint8_t *blk = (const uint8_t *)tab + (row * (E >> 5) + (e >> 5)) * 20;
-            const uint16_t dh = (uint16_t)(blk[0] | (blk[1] << 8)), mh = (uint16_t)(blk[2] | (blk[3] << 8));
-            const int i = e & 31;
-            const uint8_t byte = blk[4 + (i & 15)];
-            const int q = i < 16 ? (byte & 15) : (byte >> 4);
-            return fmaf((float)q, h2f(dh), h2f(mh));  // ggml's x*d + m, contracted by gcc -mfma
+    } else if (type == W_F16) {
+        const half8 h = *(const half8 *)((const _Float16 *)tab + row * E + e0);
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = (float)h[j];
+    } else {
+        const bool q1 = type == W_Q4_1;
+        const int bs = q1 ? 20 : 18, i0 = e0 & 31;
+        const uint8_t *blk = (const uint8_t *)tab + (row * (E >> 5) + (e0 >> 5)) * bs;
+        const float d = h2f(*(const uint16_t *)blk);
+        const float m = q1 ? h2f(*(const uint16_t *)(blk + 2)) : 0.f;
+        const uint16_t *qp = (const uint16_t *)(blk + (q1 ? 4 : 2) + (i0 & 15));  // byte i: elements i, i + 16
+        const int sh = i0 >= 16 ? 4 : 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint32_t two = qp[w];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int q = (int)((two >> (8 * k + sh)) & 15u);
+                v[2 * w + k] = q1 ? fmaf((float)q, d, m) : (float)(q - 8) * d;
+            }
         }
     }
 }
 
-template <int WT>
+// 16 rows per workgroup, four lanes per (row, 32-element block) like the GEMM
+// LayerNorm epilogue (ln_row_phase_q): values stay in registers, statistics
+// in double combined quarter -> block (shuffles) -> row (fixed block order).
+template <int WT, int NBLK>
 __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char dsm[];
-    const int E = a.E, ld = E + 4, nblk = E >> 5;
-    float *stage = (float *)dsm;
-    double *red = (double *)(dsm + (size_t)16 * ld * 4);
-    int *rinfo = (int *)(red + 2 * 16 * nblk);  // [16][2]: token, position (-1 = padding row)
+    constexpr int E = NBLK * 32, TPT = 64 * NBLK / 256;  // tasks per thread
+    __shared__ double red1[16 * NBLK], red2[16 * NBLK];
+    __shared__ int rinfo[32];  // [16][2]: token, position (-1 = padding row)
     const int tid = threadIdx.x;
     const int64_t row0 = (int64_t)blockIdx.x * 16;
     if (tid < 16) {
@@ -331,20 +281,70 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
         rinfo[2 * tid + 1] = pos;
     }
     __syncthreads();
-    for (int idx = tid; idx < 16 * E; idx += 256) {
-        const int r = idx / E, e = idx - r * E;
+    float v[TPT][8];
+#pragma unroll
+    for (int it = 0; it < TPT; it++) {
+        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, e0 = 32 * b + 8 * qq;
         const int tok = rinfo[2 * r], pos = rinfo[2 * r + 1];
-        float v = 0.f;
+        double s = 0.0;
         if (tok >= 0) {
-            const float w = table_elem(a.word, a.word_t, tok, E, e);
-            const float ty = table_elem(a.type, a.type_t, 0, E, e);
-            const float p = table_elem(a.pos, a.pos_t, pos, E, e);
-            v = p + (ty + w);
+            float w[8], ty[8], p[8];
+            table8(a.word, a.word_t, tok, E, e0, w);
+            table8(a.type, a.type_t, 0, E, e0, ty);
+            table8(a.pos, a.pos_t, pos, E, e0, p);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                v[it][j] = p[j] + (ty[j] + w[j]);
+                s += (double)v[it][j];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[it][j] = 0.f;
         }
-        stage[r * ld + e] = v;
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        if (qq == 0) red1[r * NBLK + b] = s;
     }
     __syncthreads();
-    ln_row_phase<WT, false, false>(stage, ld, E, red, row0, nullptr, a.X, a.ln_w, a.ln_b, a.eps, a.Xa, tid, 256);
+#pragma unroll
+    for (int it = 0; it < TPT; it++) {
+        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK;
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < NBLK; k++) tot += red1[r * NBLK + k];
+        const float mean = (float)(tot / E);
+        double s2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            v[it][j] = v[it][j] - mean;
+            s2 += (double)(v[it][j] * v[it][j]);
+        }
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        if (qq == 0) red2[r * NBLK + b] = s2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < TPT; it++) {
+        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < NBLK; k++) tot += red2[r * NBLK + k];
+        const float var = (float)(tot / E);
+        const float scale = 1.0f / sqrtf(var + a.eps);
+        const float4v w0 = *(const float4v *)(a.ln_w + c), w1 = *(const float4v *)(a.ln_w + c + 4);
+        const float4v b0 = *(const float4v *)(a.ln_b + c), b1 = *(const float4v *)(a.ln_b + c + 4);
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            y[j] = w0[j] * (v[it][j] * scale) + b0[j];
+            y[4 + j] = w1[j] * (v[it][4 + j] * scale) + b1[j];
+        }
+        float4v *xo = (float4v *)(a.X + (row0 + r) * (int64_t)E + c);
+        xo[0] = float4v{y[0], y[1], y[2], y[3]};
+        xo[1] = float4v{y[4], y[5], y[6], y[7]};
+        store_act_quarter<WT>(a.Xa, E, row0 + r, b, qq, y);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -825,18 +825,24 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
         }
         // soft_max over keys for query q0 + r: this lane holds keys
         // 32 kt + (j & 3) + 8 (j >> 2) + 4 hh, the partner lane (r, 1 - hh) the rest
+        // keys >= n are masked to -inf in the one partial tile; `lim` is made
+        // opaque per head so the per-element lane masks are not hoisted out of
+        // the head loop into (spilled) scalar registers
+        int lim = n - 4 * hh;
+        asm volatile("" : "+v"(lim));
         float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 4; kt++) {
             if (kt < nkt) {
-                const bool partial = 32 * kt + 32 > n;
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    float sv = S[kt][j] * a.scale;  // ggml_scale after K.Q
-                    if (partial && 32 * kt + (j & 3) + 8 * (j >> 2) + 4 * hh >= n) sv = -INFINITY;
-                    S[kt][j] = sv;
-                    mx = fmaxf(mx, sv);
+                for (int j = 0; j < 16; j++) S[kt][j] = S[kt][j] * a.scale;  // ggml_scale after K.Q
+                if (32 * kt + 32 > n) {
+#pragma unroll
+                    for (int j = 0; j < 16; j++)
+                        if (32 * kt + (j & 3) + 8 * (j >> 2) >= lim) S[kt][j] = -INFINITY;
                 }
+#pragma unroll
+                for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[kt][j]);
             }
         }
         mx = fmaxf(mx, __shfl_xor(mx, 32));
@@ -1038,39 +1044,56 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
 // Mean pool + L2 normalise for one sentence (bert.cpp:995-1006):
 // m[e] = sum_t x[t][e] * (1.0f/N); s = sum m^2 (double); len = sqrtf(s);
 // out = m * (1.0f/len).
+// Mean pooling as ggml's mul_mat by a column of 1/N (bert.cpp:995-1001), then
+// sum of squares in double, sqrtf, 1.0f/len, scale (:1002-1006).  One thread
+// per 4 columns; the token loop is unrolled 8-deep so loads are in flight
+// together (the fma chain per column stays in token order).
 __global__ __launch_bounds__(256) void pool_l2_kernel(const float *X, const int32_t *offsets, int E, float *out) {
-    __shared__ float m[1024];
     __shared__ double red[4];
-    const int s = blockIdx.x, tid = threadIdx.x;
+    const int s = blockIdx.x, tid = threadIdx.x, c = 4 * tid;
     const int beg = offsets[s], n = offsets[s + 1] - beg;
     const float invN = 1.0f / n;
-    double ss = 0.0;
-    for (int e = tid; e < E; e += 256) {
-        float acc = 0.f;
-        for (int t = 0; t < n; t++) acc = fmaf(X[(int64_t)(beg + t) * E + e], invN, acc);
-        m[e] = acc;
-        ss += (double)(acc * acc);
+    float4v acc = {0.f, 0.f, 0.f, 0.f};
+    if (c < E) {
+        const float *p = X + (int64_t)beg * E + c;
+        int t = 0;
+        for (; t + 8 <= n; t += 8) {
+            float4v x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) x[u] = *(const float4v *)(p + (int64_t)(t + u) * E);
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[j] = fmaf(x[u][j], invN, acc[j]);
+        }
+        for (; t < n; t++) {
+            const float4v x = *(const float4v *)(p + (int64_t)t * E);
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[j] = fmaf(x[j], invN, acc[j]);
+        }
     }
+    double ss = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) ss += (double)(acc[j] * acc[j]);
     for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
     if ((tid & 63) == 0) red[tid >> 6] = ss;
     __syncthreads();
     const double tot = red[0] + red[1] + red[2] + red[3];
     const float len = sqrtf((float)tot);
     const float r = 1.0f / len;
-    for (int e = tid; e < E; e += 256) out[(int64_t)s * E + e] = m[e] * r;
+    if (c < E) *(float4v *)(out + (int64_t)s * E + c) = float4v{acc[0] * r, acc[1] * r, acc[2] * r, acc[3] * r};
 }
 
 // ---------------------------------------------------------------------------
 // launchers
 template <int WT>
 static hipError_t embed_t(const EmbedArgs &a, int Mpad, hipStream_t s) {
-    const size_t smem = (size_t)16 * (a.E + 4) * 4 + (size_t)2 * 16 * (a.E / 32) * 8 + 16 * 2 * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipFuncSetAttribute((const void *)embed_ln_kernel<WT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
+    switch (a.E) {
+        case 384: hipLaunchKernelGGL((embed_ln_kernel<WT, 12>), dim3(Mpad / 16), dim3(256), 0, s, a); break;
+        case 768: hipLaunchKernelGGL((embed_ln_kernel<WT, 24>), dim3(Mpad / 16), dim3(256), 0, s, a); break;
+        case 1024: hipLaunchKernelGGL((embed_ln_kernel<WT, 32>), dim3(Mpad / 16), dim3(256), 0, s, a); break;
+        default: return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(embed_ln_kernel<WT>, dim3(Mpad / 16), dim3(256), smem, s, a);
     return hipGetLastError();
 }
 
