@@ -37,3 +37,7 @@ clean:
 	rm -rf $(BUILD)
 
 .PHONY: all oracle clean
+
+# development timing harness for the GEMM kernels (not shipped)
+$(BUILD)/gemm_bench: tools/gemm_bench.hip embedding.cpp_amd/csrc/kernels.hip embedding.cpp_amd/csrc/kernels.h
+	$(HIPCC) $(HIPFLAGS) $< -o $@

@@ -50,7 +50,7 @@ struct WPtr {
     float unscale = 1.f;
 };
 
-enum Epi : int { EPI_QKV = 0, EPI_GELU_ACT = 1, EPI_LN = 2 };
+enum Epi : int { EPI_QKV = 0, EPI_GELU_ACT = 1, EPI_LN = 2, EPI_NONE = 3 /* main-loop probe (tools/gemm_bench) */ };
 
 // Piecewise view of a 65536-entry fp16 -> fp16 table (ggml's GELU / exp
 // tables, built on the host with glibc exactly as ggml_init builds them) whose

@@ -481,10 +481,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int A_BUF = A_BYTES + (QP ? 2 * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
-    constexpr int EPI_LDS = (EPI == EPI_QKV) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
+    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
-    static_assert(EPI == EPI_QKV || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
+    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     __shared__ __attribute__((aligned(16))) uint16_t gtab[EPI == EPI_GELU_ACT ? HALF_TABLE_LDS : 8];
 
@@ -641,7 +641,14 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     //      row = m0 + rt*16 + 4g + i, columns col0 + {0, 1} with
     //      col0 = n0 + wv*WN + 32p + 2*c16; values acc[rt][2p][i], acc[rt][2p+1][i].
     const int colw = n0 + wv * WN + 2 * c16;
-    if constexpr (EPI == EPI_QKV) {
+    if constexpr (EPI == EPI_NONE) {  // keep the accumulators observable, store nothing
+        float t = 0.f;
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int j = 0; j < NTW; j++) t += acc[rt][j][0] + acc[rt][j][3];
+        if (t == 1234.5678f) args.X[tid] = t;
+    } else if constexpr (EPI == EPI_QKV) {
         // y = b + W.x in f32 (ggml), split hi = fp16(y), lo = fp16(y - hi) for the
         // attention MFMAs.  A column pair lies wholly in Q|K or in V (E % 32 == 0).
         const int E = args.N / 3;

@@ -1,0 +1,105 @@
+// Standalone timing harness for the GEMM kernels (development tool, not part
+// of libbert.so): random operands at the minilm shapes, each configuration
+// timed with hipEvents.  Build: make tools/gemm_bench ; run on the GPU box.
+#include "../embedding.cpp_amd/csrc/kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace bertamd;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+static void *dev_random(size_t bytes, uint32_t seed, int kind) {
+    std::vector<uint8_t> h(bytes);
+    uint32_t x = seed * 2654435761u + 1;
+    for (size_t i = 0; i < bytes; i++) {
+        x = x * 1664525u + 1013904223u;
+        h[i] = (uint8_t)(x >> 24);
+    }
+    if (kind == 1) {  // fp16 in a modest range: clear exponent high bits
+        uint16_t *p = (uint16_t *)h.data();
+        for (size_t i = 0; i < bytes / 2; i++) p[i] = (uint16_t)((p[i] & 0x83ff) | 0x3000);
+    }
+    void *d;
+    CK(hipMalloc(&d, bytes));
+    CK(hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice));
+    return d;
+}
+
+template <int WT, int EPI, int BN, int NW, int BM>
+static void run(const char *name, GemmArgs a, int M, int iters) {
+    const int mt = M / BM, nt = a.N / BN;
+    auto launch = [&]() {
+        hipLaunchKernelGGL((gemm_kernel<WT, EPI, BN, NW, BM>), dim3(mt * nt), dim3(NW * 64), 0, 0, a, mt, nt);
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; i++) launch();
+    CK(hipGetLastError());
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; i++) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1000.0 / iters, fl = 2.0 * M * (double)a.N * a.K;
+    printf("%-34s M=%d N=%d K=%d  %8.1f us  %6.1f TF/s (2MNK)\n", name, M, a.N, a.K, us, fl / us * 1e-6);
+    fflush(stdout);
+}
+
+int main(int argc, char **argv) {
+    const int M = 131072, E = 384, I = 1536, iters = argc > 1 ? atoi(argv[1]) : 20;
+    const int K_max = I, N_max = 3 * I;
+    GemmArgs g;
+    g.A.q = dev_random((size_t)M * K_max, 1, 0);
+    g.A.d = dev_random((size_t)M * (K_max / 32) * 4, 2, 1);
+    g.W.q = dev_random((size_t)N_max * K_max * 4, 3, 1);
+    g.W.unscale = 1.0f / 16384;
+    g.bias = (const float *)dev_random((size_t)N_max * 4, 4, 0);
+    CK(hipMemset((void *)g.bias, 0, (size_t)N_max * 4));
+    void *big;
+    CK(hipMalloc(&big, (size_t)M * N_max * 4));
+    CK(hipMemset(big, 0, (size_t)M * N_max * 4));
+    g.qk_hi = (uint16_t *)big;
+    g.qk_lo = g.qk_hi + (size_t)M * 2 * E;
+    g.vt_hi = g.qk_lo + (size_t)M * 2 * E;
+    g.vt_lo = g.vt_hi + (size_t)M * E;
+    g.ldv = M;
+    float *X;
+    CK(hipMalloc(&X, (size_t)M * E * 4));
+    CK(hipMemset(X, 0, (size_t)M * E * 4));
+    g.X = X;
+    void *oq, *od;
+    CK(hipMalloc(&oq, (size_t)M * I));
+    CK(hipMalloc(&od, (size_t)M * (I / 32) * 4));
+    g.out_act.q = oq;
+    g.out_act.d = od;
+    g.ln_w = g.bias;
+    g.ln_b = g.bias;
+    g.eps = 1e-12f;
+    g.gelu.full = (const uint16_t *)dev_random(65536 * 2, 5, 1);
+    g.gelu.compact = (const uint16_t *)dev_random(36864 * 2, 6, 1);
+    g.gelu.pos_n = 17091;
+    g.gelu.neg_n = 17705;
+    g.gelu.n_pad = 34800;
+    g.gelu.pos_identity = 1;
+
+    GemmArgs q = g; q.K = E; q.N = 3 * E;
+    GemmArgs u = g; u.K = E; u.N = I;
+    GemmArgs o = g; o.K = E; o.N = E;
+    GemmArgs d = g; d.K = I; d.N = E;
+    run<W_Q4_0, EPI_QKV, 384, 12, 128>("qkv  <384,12,128>", q, M, iters);
+    run<W_Q4_0, EPI_NONE, 384, 12, 128>("qkv  NONE <384,12,128>", q, M, iters);
+    run<W_Q4_0, EPI_GELU_ACT, 256, 8, 128>("up   <256,8,128>", u, M, iters);
+    run<W_Q4_0, EPI_NONE, 256, 8, 128>("up   NONE <256,8,128>", u, M, iters);
+    run<W_Q4_0, EPI_LN, 384, 12, 128>("o    <384,12,128>", o, M, iters);
+    run<W_Q4_0, EPI_NONE, 384, 12, 128>("o    NONE <384,12,128>", o, M, iters);
+    run<W_Q4_0, EPI_LN, 384, 12, 128>("down <384,12,128>", d, M, iters);
+    run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
+    run<W_F16, EPI_NONE, 384, 6, 64>("f16 up NONE <384,6,64>", u, M, iters);
+    return 0;
+}
