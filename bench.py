@@ -130,7 +130,7 @@ def pmc_traffic(csv_path: str, kernel_substr: str):
 # name fragments of the dominant kernels' mangled symbols (for PMC CSV lookup)
 KERNEL_SYMBOL = {
     "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "gemm_kernel<2, 1,",
-    "gemm_down_ln": "gemm_kernel<2, 2,", "attention": "attention_kernel", "embed_ln": "embed_ln_kernel",
+    "gemm_down_ln": "gemm_kernel<2, 2,", "attention": "attention_short_kernel", "embed_ln": "embed_ln_kernel",
     "pool_l2": "pool_l2_kernel",
 }
 
@@ -146,7 +146,7 @@ def main():
     ap.add_argument("--ftype", default="q4_0", choices=list(bertlib.FTYPES))
     ap.add_argument("--w-std", type=float, default=0.05)
     ap.add_argument("--model-dir", default=os.environ.get("BERT_AMD_MODEL_DIR", "/tmp/bert_amd_models"))
-    ap.add_argument("--cpu-sample", type=int, default=64, help="sentences for the CPU oracle baseline (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="sentences for the CPU oracle baseline (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--pmc-csv", default=os.environ.get("BENCH_PMC_CSV", ""))
@@ -235,7 +235,7 @@ def main():
         avg_s = prof[dominant][0] / prof[dominant][1] / 1e3
         fl = kernel_flops(dominant, B, N, hp)
         if fl:
-            peak = PEAK_FP32_MFMA_TFLOPS if (dominant == "attention" or args.ftype == "f32") else PEAK_FP16_TFLOPS
+            peak = PEAK_FP32_MFMA_TFLOPS if (args.ftype == "f32" and dominant != "attention") else PEAK_FP16_TFLOPS
             ach = fl / avg_s / 1e12
             roofline = dict(kernel=dominant, bound="mfma", achieved=round(ach, 1), peak=peak, unit="TFLOP/s",
                             frac=round(ach / peak, 4), flops_per_launch=fl)
@@ -280,9 +280,10 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "embeddings/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
-            "dtype_note": f"{args.ftype} weights dequantised to fp16 in registers, "
-                          f"{'Q8 activations dequantised to fp16, ' if args.ftype.startswith('q') else ''}"
-                          "fp16 MFMA with f32 accumulate; attention f32 MFMA; LN/softmax sums f64",
+            "dtype_note": ("Q4 weights as exact fp16 (d_w*q split hi/lo) x Q8 integer activations on fp16 MFMA, "
+                           "f32 accumulate, per-block fold with d_a (ggml vec_dot_q4_x_q8_x)" if args.ftype.startswith("q")
+                           else f"{args.ftype} GEMM on {'fp16' if args.ftype == 'f16' else 'f32'} MFMA, f32 accumulate")
+                          + "; attention split-fp16 MFMA (f32-level); LN/softmax sums f64",
             "data": "synthetic (deterministic splitmix64 token ids and weights; no checkpoints offline)",
             "config": {"workload": f"{args.shape} {args.ftype} batch={B} seq_len={N} per GPU",
                        "model": f"all-MiniLM-L6-v2 shape ({args.shape}), synthetic weights" if args.shape == "minilm"

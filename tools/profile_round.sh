@@ -1,0 +1,28 @@
+#!/bin/bash
+# One round's measurement set on the GPU box (run from the repo root):
+#   bench.py (with CPU baseline), rocprofv3 kernel-trace stats, FETCH_SIZE and
+#   WRITE_SIZE counter passes, then bench.py again with the PMC traffic folded
+#   into its roofline object.  Results under gpurun_out/round/.
+#   tools/profile_round.sh <tag>
+TAG=${1:-r01}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp BERT_AMD_MODEL_DIR=${BERT_AMD_MODEL_DIR:-/tmp/bert_amd_models}
+OUT=$PWD/gpurun_out/round
+mkdir -p "$OUT"
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] $name"
+  ( cd /tmp && timeout -k 10 "$secs" "$@" ) > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
+}
+B="$PWD/bench.py"
+step bench 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 64
+step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o $TAG -- python3 "$B" --steps 10 --warmup 3 --cpu-sample 0
+step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0
+step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0
+F=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -1)
+W=$(find "$OUT/write" -name '*counter_collection.csv' | head -1)
+step bench_pmc 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 64 --pmc-csv "$F,$W"
+tail -1 "$OUT/bench_pmc.log"
