@@ -765,40 +765,63 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
     for (int i = tid; i < a.expt.n_pad / 8; i += 256) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
 
     const int h_beg = blockIdx.x * heads_per_wg, h_end = min(h_beg + heads_per_wg, a.H);
-    for (int h = h_beg; h < h_end; h++) {
-        __syncthreads();  // previous head's LDS reads are done
-        for (int idx = tid; idx < NK * (D / 8); idx += 256) {
-            const int key = idx / (D / 8), c = (idx - key * (D / 8)) * 8;
-            uint4 kh = {0u, 0u, 0u, 0u}, kl = {0u, 0u, 0u, 0u};
+    // K and V^T tiles of the next head are prefetched into registers while the
+    // current head computes (KIT / VIT 16-byte pieces per thread and plane)
+    constexpr int KIT = NK * (D / 8) / 256, VIT = D * (NK / 8) / 256;
+    uint4 pkh[KIT], pkl[KIT];
+    half8 pvh[VIT], pvl[VIT];
+    auto fetch = [&](int h) {
+#pragma unroll
+        for (int i = 0; i < KIT; i++) {
+            const int idx = tid + 256 * i, key = idx / (D / 8), c = (idx - key * (D / 8)) * 8;
+            pkh[i] = pkl[i] = uint4{0u, 0u, 0u, 0u};
             if (key < n) {
                 const int64_t off = (int64_t)(beg + key) * E2 + E + h * D + c;
-                kh = *(const uint4 *)(a.qk_hi + off);
-                kl = *(const uint4 *)(a.qk_lo + off);
+                pkh[i] = *(const uint4 *)(a.qk_hi + off);
+                pkl[i] = *(const uint4 *)(a.qk_lo + off);
             }
-            *(uint4 *)&Kh[key * KST + c] = kh;
-            *(uint4 *)&Kl[key * KST + c] = kl;
         }
-        for (int idx = tid; idx < D * (NK / 8); idx += 256) {
-            const int d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+#pragma unroll
+        for (int i = 0; i < VIT; i++) {
+            const int idx = tid + 256 * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
             const int64_t off = (int64_t)(h * D + d) * a.ldv + beg + k8;
-            half8 vh = {}, vl = {};
+            pvh[i] = pvl[i] = half8{};
             if (k8 + 8 <= n && v_aligned) {
-                vh = *(const half8 *)(a.vt_hi + off);
-                vl = *(const half8 *)(a.vt_lo + off);
+                pvh[i] = *(const half8 *)(a.vt_hi + off);
+                pvl[i] = *(const half8 *)(a.vt_lo + off);
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; j++)
                     if (k8 + j < n) {
-                        vh[j] = ((const _Float16 *)a.vt_hi)[off + j];
-                        vl[j] = ((const _Float16 *)a.vt_lo)[off + j];
+                        pvh[i][j] = ((const _Float16 *)a.vt_hi)[off + j];
+                        pvl[i][j] = ((const _Float16 *)a.vt_lo)[off + j];
                     }
             }
+        }
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int i = 0; i < KIT; i++) {
+            const int idx = tid + 256 * i, key = idx / (D / 8), c = (idx - key * (D / 8)) * 8;
+            *(uint4 *)&Kh[key * KST + c] = pkh[i];
+            *(uint4 *)&Kl[key * KST + c] = pkl[i];
+        }
+#pragma unroll
+        for (int i = 0; i < VIT; i++) {
+            const int idx = tid + 256 * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+            const half8 vh = pvh[i], vl = pvl[i];
             *(half4v *)&Vh[d * VST + k8] = half4v{vh[0], vh[1], vh[2], vh[3]};
             *(half4v *)&Vh[d * VST + k8 + 4] = half4v{vh[4], vh[5], vh[6], vh[7]};
             *(half4v *)&Vl[d * VST + k8] = half4v{vl[0], vl[1], vl[2], vl[3]};
             *(half4v *)&Vl[d * VST + k8 + 4] = half4v{vl[4], vl[5], vl[6], vl[7]};
         }
+    };
+    if (h_beg < h_end) fetch(h_beg);
+    for (int h = h_beg; h < h_end; h++) {
+        __syncthreads();  // previous head's LDS reads are done
+        commit();
         __syncthreads();
+        if (h + 1 < h_end) fetch(h + 1);
         const int q0 = wv * 32;
         if (q0 >= n) continue;
 
