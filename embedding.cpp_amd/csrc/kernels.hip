@@ -30,6 +30,19 @@ constexpr int LDA_F = 72;    // f32  A-tile row stride (floats) = 288 B: ds_read
 __device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 
+// Four Q8 codes rint(x_j * id) packed little-endian: y + 1.5*2^23 rounds the
+// already-rounded product y = x*id to an integer (round-to-nearest-even, as
+// rintf) and leaves it, two's complement, in the low mantissa byte; two byte
+// permutes gather the four low bytes.  Exact for |y| < 2^22 (here |y| <= 127).
+__device__ __forceinline__ uint32_t q8_pack4(float x0, float x1, float x2, float x3, float id) {
+    const float M = 12582912.0f;
+    const uint32_t b0 = __float_as_uint(x0 * id + M), b1 = __float_as_uint(x1 * id + M);
+    const uint32_t b2 = __float_as_uint(x2 * id + M), b3 = __float_as_uint(x3 * id + M);
+    const uint32_t lo = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);  // bytes: b0.0, b1.0, 0, 0
+    const uint32_t hi = __builtin_amdgcn_perm(b3, b2, 0x04000c0cu);  // bytes: 0, 0, b2.0, b3.0
+    return lo | hi;
+}
+
 // ---------------------------------------------------------------------------
 // Activation block store: one 32-element block of one row, in the format the
 // next matmul consumes (ggml quantize_row_q8_0 / q8_1 AVX2 semantics:
@@ -44,15 +57,7 @@ __device__ __forceinline__ void store_act_block(const ActPtr &A, int64_t ld, int
         const float id = amax != 0.f ? 127.f / amax : 0.f;
         uint32_t pk[8];
 #pragma unroll
-        for (int w = 0; w < 8; w++) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int q = (int)rintf(v[4 * w + j] * id);
-                x |= ((uint32_t)(q & 0xff)) << (8 * j);
-            }
-            pk[w] = x;
-        }
+        for (int w = 0; w < 8; w++) pk[w] = q8_pack4(v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3], id);
         uint4 *dst = (uint4 *)((int8_t *)A.q + row * ld + blk * 32);
         dst[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
         dst[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
@@ -93,15 +98,7 @@ __device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, i
         const float id = amax != 0.f ? 127.f / amax : 0.f;
         uint32_t pk[2];
 #pragma unroll
-        for (int w = 0; w < 2; w++) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int q = (int)rintf(v[4 * w + j] * id);
-                x |= ((uint32_t)(q & 0xff)) << (8 * j);
-            }
-            pk[w] = x;
-        }
+        for (int w = 0; w < 2; w++) pk[w] = q8_pack4(v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3], id);
         *(uint2 *)((int8_t *)A.q + row * ld + blk * 32 + 8 * qq) = make_uint2(pk[0], pk[1]);
         if (qq == 0) {
             if constexpr (WT == W_Q4_0)
@@ -121,15 +118,18 @@ __device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, i
     }
 }
 
-// fp16 -> fp16 table lookup through the LDS-resident compact part (kernels.h HalfTable).
-__device__ __forceinline__ uint32_t half_table(const uint16_t *lds, const HalfTable &T, uint32_t h) {
+// ggml's fp16 GELU table through its LDS-resident compact part (kernels.h
+// HalfTable): finite h below the identity run and above the constant run read
+// LDS; the host verified every other finite entry is h itself (x >= pos_n) or
+// neg_const (compact[pos_n + neg_n]).  Branch-free; non-finite inputs (which
+// b + W.x with finite weights cannot produce) follow their sign's rule instead
+// of ggml's NaN.
+__device__ __forceinline__ uint32_t gelu_lookup(const uint16_t *lds, int pos_n, int neg_n, uint32_t h) {
     const uint32_t mag = h & 0x7fffu;
-    const bool neg = (h & 0x8000u) != 0;
-    const bool in = neg ? mag < (uint32_t)T.neg_n : mag < (uint32_t)T.pos_n;
-    const uint32_t v = lds[in ? (neg ? T.pos_n + mag : mag) : 0];
-    uint32_t r = in ? v : (neg ? T.neg_const : h);
-    if (__builtin_expect(mag >= 0x7c00u || (!neg && !in && !T.pos_identity), 0)) r = T.full[h];
-    return r;
+    const bool neg = h > 0x7fffu;
+    const uint32_t idx = neg ? (uint32_t)pos_n + min(mag, (uint32_t)neg_n) : min(mag, (uint32_t)pos_n);
+    const uint32_t v = lds[idx];
+    return (h - (uint32_t)pos_n < 0x8000u - (uint32_t)pos_n) ? h : v;  // positive, >= pos_n: identity
 }
 
 // ---------------------------------------------------------------------------
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                         const float4v v = *(const float4v *)(sp + 4 * k);
                         const float4v bb = *(const float4v *)(args.bias + n0 + c + 4 * k);
 #pragma unroll
-                        for (int j = 0; j < 4; j++) y[4 * k + j] = h2f((uint16_t)half_table(gtab, args.gelu, f2h(bb[j] + v[j])));
+                        for (int j = 0; j < 4; j++) y[4 * k + j] = h2f((uint16_t)gelu_lookup(gtab, args.gelu.pos_n, args.gelu.neg_n, f2h(bb[j] + v[j])));
                     }
                     store_act_quarter<WT>(args.out_act, args.N, row0 + r, (n0 >> 5) + b, qq, y);
                 }
@@ -937,15 +937,8 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
                 const float id = amax != 0.f ? 127.f / amax : 0.f;
                 uint32_t pk[4];
 #pragma unroll
-                for (int m = 0; m < 4; m++) {
-                    uint32_t x = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int qv = (int)rintf(o[dt][4 * m + j] * id);
-                        x |= ((uint32_t)(qv & 0xff)) << (8 * j);
-                    }
-                    pk[m] = x;
-                }
+                for (int m = 0; m < 4; m++)
+                    pk[m] = q8_pack4(o[dt][4 * m], o[dt][4 * m + 1], o[dt][4 * m + 2], o[dt][4 * m + 3], id);
                 if (q < n) {
 #pragma unroll
                     for (int m = 0; m < 4; m++) *(uint32_t *)((int8_t *)a.ctx.q + row * E + col0 + 8 * m + 4 * hh) = pk[m];

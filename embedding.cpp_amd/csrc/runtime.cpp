@@ -89,13 +89,15 @@ CompactTable compact_table(const std::vector<uint16_t> &full, bool identity_tail
     c.compact[(size_t)(c.pos_n + c.neg_n)] = (uint16_t)c.neg_const;
     for (int h = 0; h < c.pos_n; h++) c.compact[(size_t)h] = full[(size_t)h];
     for (int m = 0; m < c.neg_n; m++) c.compact[(size_t)(c.pos_n + m)] = full[(size_t)(0x8000 | m)];
-    // self-check: the device lookup rule (kernels.hip half_table) reproduces every entry
+    // self-check of the device lookup rules on every finite pattern they serve
+    // (kernels.hip gelu_lookup; soft_max's exp lookup only sees s - max <= 0)
     for (uint32_t h = 0; h < 65536; h++) {
         const uint32_t mag = h & 0x7fffu;
         const bool neg = (h & 0x8000u) != 0;
-        const bool in = neg ? mag < (uint32_t)c.neg_n : mag < (uint32_t)c.pos_n;
-        if (mag >= 0x7c00u || (!neg && !in && !c.pos_identity)) continue;  // read from the full table
-        const uint32_t v = in ? c.compact[neg ? c.pos_n + mag : mag] : (neg ? c.neg_const : h);
+        if (mag >= 0x7c00u || (!neg && !identity_tail && mag > 0)) continue;
+        uint32_t v;
+        if (neg) v = c.compact[(size_t)(c.pos_n + std::min<uint32_t>(mag, (uint32_t)c.neg_n))];
+        else v = mag >= (uint32_t)c.pos_n ? h : c.compact[mag];
         if (v != full[h]) c.pos_n = c.neg_n = 1 << 20;  // poison: load_impl reports it
     }
     return c;
