@@ -486,7 +486,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
     static_assert(EPI == EPI_QKV || EPI == EPI_NONE || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
-    __shared__ __attribute__((aligned(16))) uint16_t gtab[EPI == EPI_GELU_ACT ? HALF_TABLE_LDS : 8];
+#ifndef GELU_LDS_TABLE
+#define GELU_LDS_TABLE 1
+#endif
+    constexpr bool GT_LDS = GELU_LDS_TABLE && EPI == EPI_GELU_ACT;
+    __shared__ __attribute__((aligned(16))) uint16_t gtab[GT_LDS ? HALF_TABLE_LDS : 8];
 
     // XCD-aware tile order: linear block ids are dealt round-robin over the 8
     // XCDs; remap so that each XCD walks a contiguous range, n fastest, so the
@@ -503,7 +507,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     const int K = args.K, nkc = K / KC, nkb = K >> 5;
     const int64_t ntile0 = (n0 + wv * WN) >> 4;
     const float unscale = args.W.unscale;
-    if constexpr (EPI == EPI_GELU_ACT) {  // GELU table -> LDS (read after the main loop's barriers)
+    if constexpr (GT_LDS) {  // GELU table -> LDS (read after the main loop's barriers)
         for (int i = tid; i < args.gelu.n_pad / 8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.compact)[i];
     }
 
@@ -717,7 +721,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                         const float4v v = *(const float4v *)(sp + 4 * k);
                         const float4v bb = *(const float4v *)(args.bias + n0 + c + 4 * k);
 #pragma unroll
-                        for (int j = 0; j < 4; j++) y[4 * k + j] = h2f((uint16_t)gelu_lookup(gtab, args.gelu.pos_n, args.gelu.neg_n, f2h(bb[j] + v[j])));
+                        for (int j = 0; j < 4; j++) y[4 * k + j] = h2f((uint16_t)gelu_lookup(GT_LDS ? gtab : args.gelu.compact, args.gelu.pos_n, args.gelu.neg_n, f2h(bb[j] + v[j])));
                     }
                     store_act_quarter<WT>(args.out_act, args.N, row0 + r, (n0 >> 5) + b, qq, y);
                 }
@@ -1145,7 +1149,9 @@ template <int WT>
 static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
     if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
-        if (epi == EPI_GELU_ACT) return gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
+        if (epi == EPI_GELU_ACT)  // 12 waves (3 per SIMD) where N allows; the GELU table fills the LDS
+            return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)
+                                  : gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
         switch (a.N) {
             case 384: return gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
             case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);
