@@ -23,9 +23,13 @@ typedef float float16v __attribute__((ext_vector_type(16)));
 typedef _Float16 half4v __attribute__((ext_vector_type(4)));
 
 constexpr int BM_MAX = GEMM_BM;  // M padding unit; GEMM tiles use BM = 128, 64 or 32
-constexpr int KC = 64;       // K per main-loop chunk = two 32-element quant blocks
-constexpr int LDA_H = 80;    // fp16 A-tile row stride (halves) = 160 B: ds_read_b128 conflict-free
-constexpr int LDA_F = 72;    // f32  A-tile row stride (floats) = 288 B: ds_read_b128 conflict-free
+#ifndef GEMM_KB
+#define GEMM_KB 2
+#endif
+constexpr int KB = GEMM_KB;           // 32-element quant blocks per main-loop chunk
+constexpr int KC = 32 * KB;           // K per main-loop chunk
+constexpr int LDA_H = KC + (KB == 2 ? 16 : 8);  // fp16 A-tile row stride (halves): 160 / 272 B, ds_read_b128 conflict-free
+constexpr int LDA_F = KC + 8;         // f32 A-tile row stride (floats)
 
 __device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
@@ -430,7 +434,7 @@ __device__ __forceinline__ void a_store(const AReg &ar, char *buf, int item, flo
         dst[0] = h0;
         dst[1] = h1;
         if ((s & 1) == 0) {
-            float *sc = (float *)(buf + A_BYTES);  // [block 0, 1 of the chunk][BM]: d_a * 2^-S (exact)
+            float *sc = (float *)(buf + A_BYTES);  // [block of the chunk][BM]: d_a * 2^-S (exact)
             sc[(s >> 1) * BM + r] = ar.d * unscale;
         }
     } else if constexpr (WT == W_F16) {
@@ -478,7 +482,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
-    constexpr int A_BUF = A_BYTES + (QP ? 2 * BM * 4 : 0);
+    constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
     constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
@@ -549,7 +553,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         }
         const char *abuf = smem + (kc & 1) * A_BUF;
 #pragma unroll
-        for (int kb = 0; kb < 2; kb++) {
+        for (int kb = 0; kb < KB; kb++) {
             if constexpr (QP) {
                 // Per (row tile, n-tile): blk = A.hi + A.lo  (two MFMAs: the exact
                 // d_w-scaled block dot product, f32-accumulated), then ONE fma
@@ -568,8 +572,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                 for (int rt = 0; rt < RT; rt++)
                     if (rt * NTW <= 1) lds_a(rt);
                 float4v blk[2];
-                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb][0].hi, zero4, 0, 0, 0);
-                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb][0].lo, blk[0], 0, 0, 0);
+                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb & 1][0].hi, zero4, 0, 0, 0);
+                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb & 1][0].lo, blk[0], 0, 0, 0);
 #pragma unroll
                 for (int t = 0; t < T; t++) {
 #pragma unroll
@@ -578,9 +582,9 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                     if (t + 1 < T) {
                         const int rt1 = (t + 1) / NTW, nt1 = (t + 1) % NTW;
                         blk[(t + 1) & 1] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb][nt1].hi, zero4, 0, 0, 0);
+                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb & 1][nt1].hi, zero4, 0, 0, 0);
                         blk[(t + 1) & 1] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb][nt1].lo, blk[(t + 1) & 1], 0, 0, 0);
+                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb & 1][nt1].lo, blk[(t + 1) & 1], 0, 0, 0);
                     }
                     const int rt = t / NTW, nt = t % NTW;
 #pragma unroll
@@ -592,9 +596,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if (more) {
+                if (kc * KB + kb + 2 < nkb) {
 #pragma unroll
-                    for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + (kc + 1) * 2 + kb);
+                    for (int nt = 0; nt < NTW; nt++)
+                        wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
                 }
             } else if constexpr (WT == W_F16) {
                 half8 a[RT];
@@ -605,14 +610,14 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                 for (int nt = 0; nt < NTW; nt++)
 #pragma unroll
                     for (int rt = 0; rt < RT; rt++)
-                        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb][nt].h, acc[rt][nt], 0, 0, 0);
-                if (more) {
+                        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].h, acc[rt][nt], 0, 0, 0);
+                if (kc * KB + kb + 2 < nkb) {
 #pragma unroll
-                    for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + (kc + 1) * 2 + kb);
+                    for (int nt = 0; nt < NTW; nt++) wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
                 }
             } else {
 #pragma unroll
-                for (int nt = 0; nt < NTW; nt++) wf[0][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * 2 + kb);
+                for (int nt = 0; nt < NTW; nt++) wf[0][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb);
 #pragma unroll
                 for (int cc = 0; cc < 2; cc++) {
                     float4v a[RT];

@@ -92,11 +92,15 @@ int main(int argc, char **argv) {
     GemmArgs u = g; u.K = E; u.N = I;
     GemmArgs o = g; o.K = E; o.N = E;
     GemmArgs d = g; d.K = I; d.N = E;
-    run<W_Q4_0, EPI_GELU_ACT, 256, 8, 128>("up   <256,8,128>", u, M, iters);
-    run<W_Q4_0, EPI_GELU_ACT, 128, 4, 128>("up   <128,4,128>", u, M, iters);
-    run<W_Q4_0, EPI_GELU_ACT, 256, 4, 64>("up   <256,4,64>", u, M, iters);
-    run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   <384,12,128>", u, M, iters);
-    run<W_Q4_0, EPI_NONE, 256, 8, 128>("up   NONE <256,8,128>", u, M, iters);
-    run<W_Q4_0, EPI_NONE, 128, 4, 128>("up   NONE <128,4,128>", u, M, iters);
+    const char *which = argc > 2 ? argv[2] : "all";
+    const bool all = !strcmp(which, "all");
+    if (all) run<W_Q4_0, EPI_QKV, 384, 12, 128>("qkv  <384,12,128>", q, M, iters);
+    if (all || !strcmp(which, "none")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("qkv  NONE <384,12,128>", q, M, iters);
+    if (all) run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   <384,12,128>", u, M, iters);
+    if (all) run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
+    if (all) run<W_Q4_0, EPI_LN, 384, 12, 128>("o    <384,12,128>", o, M, iters);
+    if (all) run<W_Q4_0, EPI_LN, 384, 12, 128>("down <384,12,128>", d, M, iters);
+    if (all || !strcmp(which, "none")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
+    if (all || !strcmp(which, "none")) run<W_F16, EPI_NONE, 384, 6, 64>("f16 up NONE <384,6,64>", u, M, iters);
     return 0;
 }
