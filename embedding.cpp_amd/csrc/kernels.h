@@ -50,7 +50,13 @@ struct WPtr {
     float unscale = 1.f;
 };
 
-enum Epi : int { EPI_QKV = 0, EPI_GELU_ACT = 1, EPI_LN = 2, EPI_NONE = 3 /* main-loop probe (tools/gemm_bench) */ };
+enum Epi : int {
+    EPI_QKV = 0,       // y = b + W.x split hi/lo for attention (Q|K row-major, V transposed)
+    EPI_GELU_ACT = 1,  // gelu(b + W.x) in the next matmul's activation format
+    EPI_LN = 2,        // LN((b + W.x) + X) -> X and activation format (the workgroup owns whole rows)
+    EPI_RESID = 3,     // (b + W.x) + X -> X; LayerNorm then runs in launch_ln (rows too wide for one tile)
+    EPI_NONE = 4       // main-loop probe (tools/gemm_bench): nothing stored
+};
 
 // Piecewise view of a 65536-entry fp16 -> fp16 table (ggml's GELU / exp
 // tables, built on the host with glibc exactly as ggml_init builds them) whose
@@ -117,6 +123,9 @@ hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s);
 hipError_t launch_gemm(int wtype, int epi, int E_or_bn, const GemmArgs &a, int Mpad, hipStream_t s);
 hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs, int max_len, hipStream_t s);
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s);
+hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const float *b, float eps,
+                     const ActPtr &out, hipStream_t s);
 bool gemm_shape_supported(int epi, int N, int K);
+bool gemm_ln_fused(int wtype, int N);  // false: EPI_RESID + launch_ln
 
 }  // namespace bertamd

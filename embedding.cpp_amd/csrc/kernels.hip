@@ -351,6 +351,76 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
     }
 }
 
+// LayerNorm of X rows in place (+ activation store) for the GEMMs whose rows
+// are too wide for one workgroup (EPI_RESID), same arithmetic as the fused
+// epilogue: 16 rows per workgroup, four lanes per (row, 32-element block).
+template <int WT, int NBLK>
+__global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__restrict__ lnw,
+                                                      const float *__restrict__ lnb, float eps, ActPtr out) {
+    constexpr int E = NBLK * 32, TPT = 64 * NBLK / 256;
+    __shared__ double red1[16 * NBLK], red2[16 * NBLK];
+    const int tid = threadIdx.x;
+    const int64_t row0 = (int64_t)blockIdx.x * 16;
+    float v[TPT][8];
+#pragma unroll
+    for (int it = 0; it < TPT; it++) {
+        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+        const float4v *xp = (const float4v *)(X + (row0 + r) * (int64_t)E + c);
+        const float4v x0 = xp[0], x1 = xp[1];
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[it][j] = x0[j];
+            v[it][4 + j] = x1[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) s += (double)v[it][j];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        if (qq == 0) red1[r * NBLK + b] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < TPT; it++) {
+        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK;
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < NBLK; k++) tot += red1[r * NBLK + k];
+        const float mean = (float)(tot / E);
+        double s2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            v[it][j] = v[it][j] - mean;
+            s2 += (double)(v[it][j] * v[it][j]);
+        }
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        if (qq == 0) red2[r * NBLK + b] = s2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < TPT; it++) {
+        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < NBLK; k++) tot += red2[r * NBLK + k];
+        const float var = (float)(tot / E);
+        const float scale = 1.0f / sqrtf(var + eps);
+        const float4v w0 = *(const float4v *)(lnw + c), w1 = *(const float4v *)(lnw + c + 4);
+        const float4v b0 = *(const float4v *)(lnb + c), b1 = *(const float4v *)(lnb + c + 4);
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            y[j] = w0[j] * (v[it][j] * scale) + b0[j];
+            y[4 + j] = w1[j] * (v[it][4 + j] * scale) + b1[j];
+        }
+        float4v *xo = (float4v *)(X + (row0 + r) * (int64_t)E + c);
+        xo[0] = float4v{y[0], y[1], y[2], y[3]};
+        xo[1] = float4v{y[4], y[5], y[6], y[7]};
+        store_act_quarter<WT>(out, E, row0 + r, b, qq, y);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // GEMM: C[M][N] = A[M][K] . W[N][K]^T on MFMA, fused epilogues.
 //
@@ -485,10 +555,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
-    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
+    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
-    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
+    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 #ifndef GELU_LDS_TABLE
 #define GELU_LDS_TABLE 1
@@ -657,6 +727,20 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
 #pragma unroll
             for (int j = 0; j < NTW; j++) t += acc[rt][j][0] + acc[rt][j][3];
         if (t == 1234.5678f) args.X[tid] = t;
+    } else if constexpr (EPI == EPI_RESID) {  // X = (b + W.x) + X, in registers
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            const int col = colw + 32 * p;
+            const float2v b = *(const float2v *)(args.bias + col);
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    float2v *xp = (float2v *)(args.X + (m0 + rt * 16 + 4 * g + i) * args.N + col);
+                    const float2v x = *xp;
+                    *xp = float2v{(b[0] + acc[rt][2 * p][i]) + x[0], (b[1] + acc[rt][2 * p + 1][i]) + x[1]};
+                }
+        }
     } else if constexpr (EPI == EPI_QKV) {
         // y = b + W.x in f32 (ggml), split hi = fp16(y), lo = fp16(y - hi) for the
         // attention MFMAs.  A column pair lies wholly in Q|K or in V (E % 32 == 0).
@@ -757,6 +841,100 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
 // f32 rounding only).  The context is quantised to the O-projection's
 // activation format in registers.
 
+// Shared pieces of the two attention kernels (32 queries per wave, lane
+// (r, hh) = query r, key / dimension half hh of the 32x32 MFMA layout).
+// S^T tile (32 keys from LDS row k0 x this wave's 32 queries), split-fp16.
+template <int D>
+__device__ __forceinline__ float16v attn_qk(const _Float16 *Kh, const _Float16 *Kl, int kst, int k0, int r, int hh,
+                                            const half8 *qh, const half8 *ql) {
+    float16v S = {};
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ks++) {
+        const int off = (k0 + r) * kst + 16 * ks + 8 * hh;
+        const half8 kh = *(const half8 *)&Kh[off], kl = *(const half8 *)&Kl[off];
+        S = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], S, 0, 0, 0);
+        S = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], S, 0, 0, 0);
+        S = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], S, 0, 0, 0);
+    }
+    return S;
+}
+
+// o += V^T . P^T for 32 keys from LDS column k0 (P = the tile's fp16 table
+// values, exact): k-step ks, B element j of lane half hh is key
+// k0 + 16 ks + 8 (j >> 2) + 4 hh + (j & 3) = register 8 ks + j of the S tile.
+template <int D>
+__device__ __forceinline__ void attn_pv(float16v *o, const _Float16 *Vh, const _Float16 *Vl, int vst, int k0, int r,
+                                        int hh, const float16v &P) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+        half8 ph;
+#pragma unroll
+        for (int j = 0; j < 8; j++) ph[j] = (_Float16)P[8 * ks + j];
+        const int key = k0 + 16 * ks + 4 * hh;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; dt++) {
+            const int off = (dt * 32 + r) * vst + key;
+            const half4v h0 = *(const half4v *)&Vh[off], h1 = *(const half4v *)&Vh[off + 8];
+            const half4v l0 = *(const half4v *)&Vl[off], l1 = *(const half4v *)&Vl[off + 8];
+            const half8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+            const half8 vl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[dt], 0, 0, 0);
+        }
+    }
+}
+
+// ctx = o * (float)(1/sum), stored in the O-projection's activation format:
+// lane (r, hh) holds ctx[row][h D + 32 dt + (j & 3) + 8 (j >> 2) + 4 hh], one
+// 32-value quant block per (query, dt) split over the lane pair (r, hh).
+template <int WT, int D>
+__device__ __forceinline__ void attn_store_ctx(const AttnArgs &a, float16v *o, float rs, int64_t row, bool valid,
+                                               int h, int hh) {
+    const int E = a.E;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; dt++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) o[dt][j] *= rs;
+        const int col0 = h * D + dt * 32;
+        if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+            float amax = 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; j++) amax = fmaxf(amax, fabsf(o[dt][j]));
+            amax = fmaxf(amax, __shfl_xor(amax, 32));
+            const float d = amax / 127.f;
+            const float id = amax != 0.f ? 127.f / amax : 0.f;
+            uint32_t pk[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+                pk[m] = q8_pack4(o[dt][4 * m], o[dt][4 * m + 1], o[dt][4 * m + 2], o[dt][4 * m + 3], id);
+            if (valid) {
+#pragma unroll
+                for (int m = 0; m < 4; m++) *(uint32_t *)((int8_t *)a.ctx.q + row * E + col0 + 8 * m + 4 * hh) = pk[m];
+                if (hh == 0) {
+                    const int64_t bi = row * (E >> 5) + (col0 >> 5);
+                    if constexpr (WT == W_Q4_0)
+                        ((uint16_t *)a.ctx.d)[bi] = f2h(d);
+                    else
+                        ((float *)a.ctx.d)[bi] = d;
+                }
+            }
+        } else if (valid) {
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const int col = col0 + 8 * m + 4 * hh;
+                if constexpr (WT == W_F16) {
+                    *(half4v *)((_Float16 *)a.ctx.q + row * E + col) =
+                        half4v{(_Float16)o[dt][4 * m], (_Float16)o[dt][4 * m + 1], (_Float16)o[dt][4 * m + 2],
+                               (_Float16)o[dt][4 * m + 3]};
+                } else {
+                    *(float4v *)((float *)a.ctx.q + row * E + col) =
+                        float4v{o[dt][4 * m], o[dt][4 * m + 1], o[dt][4 * m + 2], o[dt][4 * m + 3]};
+                }
+            }
+        }
+    }
+}
+
 template <int WT, int D>
 __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int heads_per_wg) {
     constexpr int NK = 128;      // keys staged (n <= 128)
@@ -849,19 +1027,7 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
         float16v S[4];
         const float16v zero16 = {};
 #pragma unroll
-        for (int kt = 0; kt < 4; kt++) {
-            S[kt] = zero16;
-            if (kt < nkt) {
-#pragma unroll
-                for (int ks = 0; ks < D / 16; ks++) {
-                    const int off = (kt * 32 + r) * KST + 16 * ks + 8 * hh;
-                    const half8 kh = *(const half8 *)&Kh[off], kl = *(const half8 *)&Kl[off];
-                    S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], S[kt], 0, 0, 0);
-                    S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], S[kt], 0, 0, 0);
-                    S[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], S[kt], 0, 0, 0);
-                }
-            }
-        }
+        for (int kt = 0; kt < 4; kt++) S[kt] = kt < nkt ? attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql) : zero16;
         // soft_max over keys for query q0 + r: this lane holds keys
         // 32 kt + (j & 3) + 8 (j >> 2) + 4 hh, the partner lane (r, 1 - hh) the rest
         // keys >= n are masked to -inf in the one partial tile; `lim` is made
@@ -901,175 +1067,144 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
         }
         sum += __shfl_xor(sum, 32);
         const float rs = (float)(1.0 / sum);
-        // ctx^T = V^T . P^T.  k-step ks of key tile kt: B element j of lane half hh
-        // is key 32 kt + 16 ks + 8 (j >> 2) + 4 hh + (j & 3) = register 8 ks + j.
         float16v o[D / 32];
 #pragma unroll
         for (int dt = 0; dt < D / 32; dt++) o[dt] = zero16;
 #pragma unroll
-        for (int kt = 0; kt < 4; kt++) {
-            if (kt < nkt) {
-#pragma unroll
-                for (int ks = 0; ks < 2; ks++) {
-                    half8 ph;
-#pragma unroll
-                    for (int j = 0; j < 8; j++) ph[j] = (_Float16)S[kt][8 * ks + j];  // exact: fp16 table values
-                    const int key = kt * 32 + 16 * ks + 4 * hh;
-#pragma unroll
-                    for (int dt = 0; dt < D / 32; dt++) {
-                        const int off = (dt * 32 + r) * VST + key;
-                        const half4v h0 = *(const half4v *)&Vh[off], h1 = *(const half4v *)&Vh[off + 8];
-                        const half4v l0 = *(const half4v *)&Vl[off], l1 = *(const half4v *)&Vl[off + 8];
-                        const half8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-                        const half8 vl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
-                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
-                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[dt], 0, 0, 0);
-                    }
-                }
-            }
-        }
-        // lane (r, hh) holds ctx[q0 + r][h D + 32 dt + (j & 3) + 8 (j >> 2) + 4 hh]:
-        // one 32-value quant block per (query, dt), split over the lane pair (r, hh).
-        const int q = q0 + r;
-        const int64_t row = beg + q;
-#pragma unroll
-        for (int dt = 0; dt < D / 32; dt++) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) o[dt][j] *= rs;
-            const int col0 = h * D + dt * 32;
-            if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
-                float amax = 0.f;
-#pragma unroll
-                for (int j = 0; j < 16; j++) amax = fmaxf(amax, fabsf(o[dt][j]));
-                amax = fmaxf(amax, __shfl_xor(amax, 32));
-                const float d = amax / 127.f;
-                const float id = amax != 0.f ? 127.f / amax : 0.f;
-                uint32_t pk[4];
-#pragma unroll
-                for (int m = 0; m < 4; m++)
-                    pk[m] = q8_pack4(o[dt][4 * m], o[dt][4 * m + 1], o[dt][4 * m + 2], o[dt][4 * m + 3], id);
-                if (q < n) {
-#pragma unroll
-                    for (int m = 0; m < 4; m++) *(uint32_t *)((int8_t *)a.ctx.q + row * E + col0 + 8 * m + 4 * hh) = pk[m];
-                    if (hh == 0) {
-                        const int64_t bi = row * (E >> 5) + (col0 >> 5);
-                        if constexpr (WT == W_Q4_0) {
-                            ((uint16_t *)a.ctx.d)[bi] = f2h(d);
-                        } else {
-                            ((float *)a.ctx.d)[bi] = d;
-                        }
-                    }
-                }
-            } else if (q < n) {
-#pragma unroll
-                for (int m = 0; m < 4; m++) {
-                    const int col = col0 + 8 * m + 4 * hh;
-                    if constexpr (WT == W_F16) {
-                        *(half4v *)((_Float16 *)a.ctx.q + row * E + col) =
-                            half4v{(_Float16)o[dt][4 * m], (_Float16)o[dt][4 * m + 1], (_Float16)o[dt][4 * m + 2],
-                                   (_Float16)o[dt][4 * m + 3]};
-                    } else {
-                        *(float4v *)((float *)a.ctx.q + row * E + col) =
-                            float4v{o[dt][4 * m], o[dt][4 * m + 1], o[dt][4 * m + 2], o[dt][4 * m + 3]};
-                    }
-                }
-            }
-        }
+        for (int kt = 0; kt < 4; kt++)
+            if (kt < nkt) attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S[kt]);
+        attn_store_ctx<WT, D>(a, o, rs, beg + q0 + r, q0 + r < n, h, hh);
     }
 }
 
-// Attention for 128 < n <= 512 (f32 MFMA on the reconstructed hi + lo values;
-// scores through LDS).  One workgroup per (64 queries, head, sentence).
+// Attention for 128 < n <= 512: one workgroup per (128-query block, head,
+// sentence), wave w owning queries 32w..32w+31 of the block.  Keys stream
+// through LDS in 128-key chunks, twice: pass 1 finds every query's maximum
+// score; pass 2 recomputes the identical scores (same MFMA sequence) for
+// p = exp_tab[fp16(s - max)], the exact double sum and P.V.  So ggml's
+// soft_max (global max first) holds without materialising the n x n scores.
 template <int WT, int D>
 __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char dsm[];
-    const int s = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * ATT_QB;
+    constexpr int NK = 128, KST = D + 8, VST = NK + 4;
+    __shared__ __attribute__((aligned(16))) _Float16 Kh[NK * KST], Kl[NK * KST], Vh[D * VST], Vl[D * VST];
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
+    const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
     const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
-    if (q0 >= n || n <= 128) return;  // n <= 128: attention_short_kernel
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4, c16 = lane & 15;
+    if (n <= NK || qb * NK >= n) return;  // n <= 128: attention_short_kernel
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
     const int E = a.E, E2 = 2 * E;
-    const int nk16 = (n + 15) & ~15;
-    const int LDS_S = ((nk16 + 55) / 64) * 64 + 8;  // == 8 (mod 64) dwords: conflict-free float4 row reads
-    float *S = (float *)dsm + wv * 16 * LDS_S;
-    const int qw0 = q0 + wv * 16;  // this wave's first query
+    const bool v_aligned = (beg & 7) == 0;
+    const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
+    for (int i = tid; i < a.expt.n_pad / 8; i += 256) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
 
-    auto ld4 = [&](int64_t off) {  // hi + lo of four consecutive Q|K values
-        const half4v hv = *(const half4v *)((const _Float16 *)a.qk_hi + off), lv = *(const half4v *)((const _Float16 *)a.qk_lo + off);
-        return float4v{(float)hv[0] + (float)lv[0], (float)hv[1] + (float)lv[1], (float)hv[2] + (float)lv[2],
-                       (float)hv[3] + (float)lv[3]};
+    const int q0 = qb * NK + wv * 32;
+    const bool active = q0 < n;  // wave-uniform
+    half8 qh[D / 16], ql[D / 16];
+    {
+        const int qr = min(q0 + r, n - 1);
+        const int64_t off = (int64_t)(beg + qr) * E2 + h * D + 8 * hh;
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ks++) {
+            qh[ks] = *(const half8 *)(a.qk_hi + off + 16 * ks);
+            ql[ks] = *(const half8 *)(a.qk_lo + off + 16 * ks);
+        }
+    }
+    auto stage = [&](int c, bool with_v) {
+        const int kbase = c * NK;
+        for (int idx = tid; idx < NK * (D / 8); idx += 256) {
+            const int key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
+            uint4 kh = {0u, 0u, 0u, 0u}, kl = {0u, 0u, 0u, 0u};
+            if (kbase + key < n) {
+                const int64_t off = (int64_t)(beg + kbase + key) * E2 + E + h * D + col;
+                kh = *(const uint4 *)(a.qk_hi + off);
+                kl = *(const uint4 *)(a.qk_lo + off);
+            }
+            *(uint4 *)&Kh[key * KST + col] = kh;
+            *(uint4 *)&Kl[key * KST + col] = kl;
+        }
+        if (!with_v) return;
+        for (int idx = tid; idx < D * (NK / 8); idx += 256) {
+            const int d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+            const int64_t off = (int64_t)(h * D + d) * a.ldv + beg + kbase + k8;
+            half8 vh = {}, vl = {};
+            if (kbase + k8 + 8 <= n && v_aligned) {
+                vh = *(const half8 *)(a.vt_hi + off);
+                vl = *(const half8 *)(a.vt_lo + off);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (kbase + k8 + j < n) {
+                        vh[j] = ((const _Float16 *)a.vt_hi)[off + j];
+                        vl[j] = ((const _Float16 *)a.vt_lo)[off + j];
+                    }
+            }
+            *(half4v *)&Vh[d * VST + k8] = half4v{vh[0], vh[1], vh[2], vh[3]};
+            *(half4v *)&Vh[d * VST + k8 + 4] = half4v{vh[4], vh[5], vh[6], vh[7]};
+            *(half4v *)&Vl[d * VST + k8] = half4v{vl[0], vl[1], vl[2], vl[3]};
+            *(half4v *)&Vl[d * VST + k8 + 4] = half4v{vl[4], vl[5], vl[6], vl[7]};
+        }
     };
-    float4v qf[D / 16];
-    {
-        const int qr = min(qw0 + c16, n - 1);
+    // scaled, masked scores of the 32-key tile starting at absolute key k0
+    int lim = n - 4 * hh;
+    asm volatile("" : "+v"(lim));
+    auto scores = [&](int k0, int kl0) {
+        float16v S = attn_qk<D>(Kh, Kl, KST, kl0, r, hh, qh, ql);
 #pragma unroll
-        for (int c = 0; c < D / 16; c++) qf[c] = ld4((int64_t)(beg + qr) * E2 + h * D + 16 * c + 4 * g);
-    }
-    for (int key0 = 0; key0 < n; key0 += 16) {
-        const int kr = min(key0 + c16, n - 1);
-        float4v acc = {0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 16; j++) S[j] = S[j] * a.scale;  // ggml_scale after K.Q
+        if (k0 + 32 > n) {
 #pragma unroll
-        for (int c = 0; c < D / 16; c++) {
-            const float4v kf = ld4((int64_t)(beg + kr) * E2 + E + h * D + 16 * c + 4 * g);
-#pragma unroll
-            for (int j = 0; j < 4; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[c][j], kf[j], acc, 0, 0, 0);
+            for (int j = 0; j < 16; j++)
+                if (k0 + (j & 3) + 8 * (j >> 2) >= lim) S[j] = -INFINITY;
         }
+        return S;
+    };
+    const int nch = (n + NK - 1) / NK;
+    float mx = -INFINITY;
+    for (int c = 0; c < nch; c++) {  // pass 1: maxima
+        __syncthreads();
+        stage(c, false);
+        __syncthreads();
+        if (active) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) S[(g * 4 + i) * LDS_S + key0 + c16] = acc[i] * a.scale;
-    }
-    __syncthreads();
-    {
-        const int rr = lane >> 2, part = lane & 3;
-        float *row = S + rr * LDS_S;
-        float mx = -INFINITY;
-        for (int k = part; k < n; k += 4) mx = fmaxf(mx, row[k]);
-        mx = fmaxf(mx, __shfl_xor(mx, 1));
-        mx = fmaxf(mx, __shfl_xor(mx, 2));
-        double sum = 0.0;
-        for (int k = part; k < n; k += 4) {
-            const float p = h2f(a.expt.full[f2h(row[k] - mx)]);
-            row[k] = p;
-            sum += (double)p;
-        }
-        sum += __shfl_xor(sum, 1);
-        sum += __shfl_xor(sum, 2);
-        const float r = (float)(1.0 / sum);
-        for (int k = part; k < n; k += 4) row[k] = row[k] * r;
-        for (int k = n + part; k < nk16; k += 4) row[k] = 0.f;
-    }
-    __syncthreads();
-    float4v o[D / 16];
+            for (int kt = 0; kt < NK / 32; kt++) {
+                const int k0 = c * NK + 32 * kt;
+                if (k0 < n) {
+                    const float16v S = scores(k0, 32 * kt);
 #pragma unroll
-    for (int dt = 0; dt < D / 16; dt++) o[dt] = float4v{0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nk16; kc += 16) {
-        const float4v pf = *(const float4v *)(S + c16 * LDS_S + kc + 4 * g);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int vr = min(kc + 4 * g + j, n - 1);
-#pragma unroll
-            for (int dt = 0; dt < D / 16; dt++) {
-                const int64_t vo = (int64_t)(h * D + dt * 16 + c16) * a.ldv + beg + vr;
-                const float vv = h2f(a.vt_hi[vo]) + h2f(a.vt_lo[vo]);
-                o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[j], vv, o[dt], 0, 0, 0);
+                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
+                }
             }
         }
     }
-    __syncthreads();
-    float *T = S;  // reuse: [16][D + 4]
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    double sum = 0.0;
+    float16v o[D / 32];
 #pragma unroll
-    for (int dt = 0; dt < D / 16; dt++)
+    for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
+    for (int c = 0; c < nch; c++) {  // pass 2: p, sum, P.V
+        __syncthreads();
+        stage(c, true);
+        __syncthreads();
+        if (active) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) T[(g * 4 + i) * (D + 4) + dt * 16 + c16] = o[dt][i];
-    __syncthreads();
-    if (lane < 16 * (D / 32)) {
-        const int rr = lane / (D / 32), blk = lane % (D / 32);
-        const int q = qw0 + rr;
-        if (q < n) {
-            float v[32];
+            for (int kt = 0; kt < NK / 32; kt++) {
+                const int k0 = c * NK + 32 * kt;
+                if (k0 < n) {
+                    float16v S = scores(k0, 32 * kt);
 #pragma unroll
-            for (int j = 0; j < 32; j++) v[j] = T[rr * (D + 4) + blk * 32 + j];
-            store_act_block<WT>(a.ctx, E, beg + q, h * (D / 32) + blk, v);
+                    for (int j = 0; j < 16; j++) {
+                        const uint32_t hm = f2h(S[j] - mx) & 0x7fffu;  // s - max <= 0; -inf -> 0
+                        const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
+                        S[j] = p;
+                        sum += (double)p;
+                    }
+                    attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
+                }
+            }
         }
     }
+    sum += __shfl_xor(sum, 32);
+    if (active) attn_store_ctx<WT, D>(a, o, (float)(1.0 / sum), beg + q0 + r, q0 + r < n, h, hh);
 }
 
 // ---------------------------------------------------------------------------
@@ -1157,11 +1292,8 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
         if (epi == EPI_GELU_ACT)  // 12 waves (3 per SIMD) where N allows; the GELU table fills the LDS
             return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)
                                   : gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
-        switch (a.N) {
-            case 384: return gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
-            case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);
-            case 1024: return gemm_t<WT, EPI_LN, 1024, 16, 32>(a, Mpad, s);
-        }
+        if (epi == EPI_LN && a.N == 384) return gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
+        if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
     } else {
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 6, 64>(a, Mpad, s);
         if (epi == EPI_GELU_ACT) return gemm_t<WT, EPI_GELU_ACT, 256, 4, 64>(a, Mpad, s);
@@ -1174,10 +1306,18 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+// Q4 weights: a 12-wave workgroup owns whole 384-wide rows; wider rows would
+// spill (two W blocks in flight x hi/lo), so they add the residual in the GEMM
+// and normalise in launch_ln.  F16 / F32 fuse LN up to 1024.
+bool gemm_ln_fused(int wtype, int N) {
+    if (wtype == W_Q4_0 || wtype == W_Q4_1) return N == 384;
+    return N == 384 || N == 768 || N == 1024;
+}
+
 bool gemm_shape_supported(int epi, int N, int K) {
     if (K % KC) return false;
     if (epi == EPI_QKV) return N % 384 == 0;
-    if (epi == EPI_GELU_ACT) return N % 256 == 0;
+    if (epi == EPI_GELU_ACT || epi == EPI_RESID) return N % 256 == 0;
     return N == 384 || N == 768 || N == 1024;
 }
 
@@ -1201,17 +1341,7 @@ static hipError_t attn_t(const AttnArgs &a, int n_seqs, int max_len, hipStream_t
     hipLaunchKernelGGL((attention_short_kernel<WT, D>), dim3(groups, n_seqs), dim3(256), 0, s, a, hpw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || max_len <= 128) return e;
-    const int nk16 = (max_len + 15) & ~15;
-    const int lds_s = ((nk16 + 55) / 64) * 64 + 8;
-    const size_t smem = (size_t)4 * 16 * lds_s * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipFuncSetAttribute((const void *)attention_long_kernel<WT, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-        attr_set = true;
-    }
-    hipLaunchKernelGGL((attention_long_kernel<WT, D>), dim3((max_len + ATT_QB - 1) / ATT_QB, a.H, n_seqs), dim3(256),
-                       smem, s, a);
+    hipLaunchKernelGGL((attention_long_kernel<WT, D>), dim3((max_len + 127) / 128, a.H, n_seqs), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -1229,6 +1359,29 @@ hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs
         case W_F16: return attn_w<W_F16>(d_head, a, n_seqs, max_len, s);
         case W_Q4_0: return attn_w<W_Q4_0>(d_head, a, n_seqs, max_len, s);
         case W_Q4_1: return attn_w<W_Q4_1>(d_head, a, n_seqs, max_len, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int WT>
+static hipError_t ln_w(float *X, int Mpad, int E, const float *w, const float *b, float eps, const ActPtr &out,
+                       hipStream_t s) {
+    switch (E) {
+        case 384: hipLaunchKernelGGL((ln_rows_kernel<WT, 12>), dim3(Mpad / 16), dim3(256), 0, s, X, w, b, eps, out); break;
+        case 768: hipLaunchKernelGGL((ln_rows_kernel<WT, 24>), dim3(Mpad / 16), dim3(256), 0, s, X, w, b, eps, out); break;
+        case 1024: hipLaunchKernelGGL((ln_rows_kernel<WT, 32>), dim3(Mpad / 16), dim3(256), 0, s, X, w, b, eps, out); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const float *b, float eps,
+                     const ActPtr &out, hipStream_t s) {
+    switch (wtype) {
+        case W_F32: return ln_w<W_F32>(X, Mpad, E, w, b, eps, out, s);
+        case W_F16: return ln_w<W_F16>(X, Mpad, E, w, b, eps, out, s);
+        case W_Q4_0: return ln_w<W_Q4_0>(X, Mpad, E, w, b, eps, out, s);
+        case W_Q4_1: return ln_w<W_Q4_1>(X, Mpad, E, w, b, eps, out, s);
     }
     return hipErrorInvalidValue;
 }

@@ -423,6 +423,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     if (!ensure_workspace(ctx, R, Mpad, n_seqs)) return false;
     Workspace &w = R.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
+    const bool ln_fused = gemm_ln_fused(wt, E);
 
     EmbedArgs ea;
     ea.tokens = d_tok;
@@ -485,7 +486,12 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         o.ln_w = L.ln1_w;
         o.ln_b = L.ln1_b;
         o.eps = hp.eps;
-        LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)Mpad, st));
+        if (ln_fused) {
+            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)Mpad, st));
+        } else {
+            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)Mpad, st));
+            LAUNCH_OK("ln", launch_ln(wt, w.X, (int)Mpad, E, L.ln1_w, L.ln1_b, hp.eps, w.Xa, st));
+        }
 
         GemmArgs u;
         u.A = w.Xa;
@@ -508,7 +514,12 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         dn.ln_w = L.ln2_w;
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
-        LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)Mpad, st));
+        if (ln_fused) {
+            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)Mpad, st));
+        } else {
+            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)Mpad, st));
+            LAUNCH_OK("ln", launch_ln(wt, w.X, (int)Mpad, E, L.ln2_w, L.ln2_b, hp.eps, w.Xa, st));
+        }
     }
     LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st));
     return true;
@@ -723,7 +734,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     ctx->type_t = hm.type->type;
     const int D = (int)(E / hp.n_head);
     if ((E != 384 && E != 768 && E != 1024) || (D != 32 && D != 64) || I % 256 || hp.n_max_tokens > 512 ||
-        !gemm_shape_supported(EPI_QKV, (int)(3 * E), (int)E) || !gemm_shape_supported(EPI_LN, (int)E, (int)I)) {
+        !gemm_shape_supported(EPI_QKV, (int)(3 * E), (int)E) || !gemm_shape_supported(gemm_ln_fused(ctx->wtype, (int)E) ? EPI_LN : EPI_RESID, (int)E, (int)I)) {
         set_err("unsupported shape: n_embd=%d n_head=%d n_intermediate=%d n_max_tokens=%d", hp.n_embd, hp.n_head,
                 hp.n_intermediate, hp.n_max_tokens);
         return nullptr;
