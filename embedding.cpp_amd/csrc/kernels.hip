@@ -1294,6 +1294,16 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
                                   : gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
         if (epi == EPI_LN && a.N == 384) return gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
+    } else if constexpr (WT == W_F16) {  // tools/gemm_bench: 12-wave 384-column tiles win by 1.4-1.9x
+        if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
+        if (epi == EPI_GELU_ACT)
+            return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)
+                                  : gemm_t<WT, EPI_GELU_ACT, 256, 4, 64>(a, Mpad, s);
+        switch (a.N) {
+            case 384: return gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
+            case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);
+            case 1024: return gemm_t<WT, EPI_LN, 1024, 8, 32>(a, Mpad, s);
+        }
     } else {
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 6, 64>(a, Mpad, s);
         if (epi == EPI_GELU_ACT) return gemm_t<WT, EPI_GELU_ACT, 256, 4, 64>(a, Mpad, s);

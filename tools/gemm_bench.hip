@@ -55,8 +55,13 @@ int main(int argc, char **argv) {
     const int M = 131072, E = 384, I = 1536, iters = argc > 1 ? atoi(argv[1]) : 20;
     const int K_max = I, N_max = 3 * I;
     GemmArgs g;
-    g.A.q = dev_random((size_t)M * K_max, 1, 0);
-    g.A.d = dev_random((size_t)M * (K_max / 32) * 4, 2, 1);
+    {   // activations: sized for the largest K (3072) in the widest format used (fp16); values irrelevant
+        void *aq;
+        CK(hipMalloc(&aq, (size_t)M * 3072 * 4));
+        CK(hipMemset(aq, 0x11, (size_t)M * 3072 * 4));
+        g.A.q = aq;
+    }
+    g.A.d = dev_random((size_t)M * (3072 / 32) * 4, 2, 1);
     g.W.q = dev_random((size_t)N_max * K_max * 4, 3, 1);
     g.W.unscale = 1.0f / 16384;
     g.bias = (const float *)dev_random((size_t)N_max * 4, 4, 0);
@@ -70,12 +75,12 @@ int main(int argc, char **argv) {
     g.vt_lo = g.vt_hi + (size_t)M * E;
     g.ldv = M;
     float *X;
-    CK(hipMalloc(&X, (size_t)M * E * 4));
-    CK(hipMemset(X, 0, (size_t)M * E * 4));
+    CK(hipMalloc(&X, (size_t)M * 1024 * 4));
+    CK(hipMemset(X, 0, (size_t)M * 1024 * 4));
     g.X = X;
     void *oq, *od;
-    CK(hipMalloc(&oq, (size_t)M * I));
-    CK(hipMalloc(&od, (size_t)M * (I / 32) * 4));
+    CK(hipMalloc(&oq, (size_t)M * 3072 * 4));  // largest activation output used below (f32-sized)
+    CK(hipMalloc(&od, (size_t)M * (3072 / 32) * 4));
     g.out_act.q = oq;
     g.out_act.d = od;
     g.ln_w = g.bias;
@@ -94,13 +99,24 @@ int main(int argc, char **argv) {
     GemmArgs d = g; d.K = I; d.N = E;
     const char *which = argc > 2 ? argv[2] : "all";
     const bool all = !strcmp(which, "all");
-    if (all) run<W_Q4_0, EPI_QKV, 384, 12, 128>("qkv  <384,12,128>", q, M, iters);
     if (all || !strcmp(which, "none")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("qkv  NONE <384,12,128>", q, M, iters);
-    if (all) run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   <384,12,128>", u, M, iters);
-    if (all) run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
-    if (all) run<W_Q4_0, EPI_LN, 384, 12, 128>("o    <384,12,128>", o, M, iters);
-    if (all) run<W_Q4_0, EPI_LN, 384, 12, 128>("down <384,12,128>", d, M, iters);
     if (all || !strcmp(which, "none")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
-    if (all || !strcmp(which, "none")) run<W_F16, EPI_NONE, 384, 6, 64>("f16 up NONE <384,6,64>", u, M, iters);
+    if (all || !strcmp(which, "f16")) {
+        // e5-base shapes on F16 weights (C4): E = 768, I = 3072
+        GemmArgs q2 = g; q2.K = 768; q2.N = 2304;
+        GemmArgs u2 = g; u2.K = 768; u2.N = 3072;
+        GemmArgs d2 = g; d2.K = 3072; d2.N = 768;
+        const int M2 = 65536;
+        run<W_F16, EPI_QKV, 384, 6, 64>("f16 qkv <384,6,64>", q2, M2, iters);
+        run<W_F16, EPI_QKV, 384, 12, 128>("f16 qkv <384,12,128>", q2, M2, iters);
+        run<W_F16, EPI_QKV, 256, 4, 128>("f16 qkv <256,4,128>", q2, M2, iters);
+        run<W_F16, EPI_GELU_ACT, 256, 4, 64>("f16 up <256,4,64>", u2, M2, iters);
+        run<W_F16, EPI_GELU_ACT, 384, 12, 128>("f16 up <384,12,128>", u2, M2, iters);
+        run<W_F16, EPI_GELU_ACT, 384, 6, 128>("f16 up <384,6,128>", u2, M2, iters);
+        run<W_F16, EPI_LN, 768, 12, 64>("f16 down <768,12,64>", d2, M2, iters);
+        run<W_F16, EPI_NONE, 768, 12, 64>("f16 down NONE <768,12,64>", d2, M2, iters);
+        run<W_F16, EPI_RESID, 256, 4, 128>("f16 down RESID <256,4,128>", d2, M2, iters);
+        run<W_F16, EPI_RESID, 384, 6, 128>("f16 down RESID <384,6,128>", d2, M2, iters);
+    }
     return 0;
 }
