@@ -1109,35 +1109,55 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
             ql[ks] = *(const half8 *)(a.qk_lo + off + 16 * ks);
         }
     }
-    auto stage = [&](int c, bool with_v) {
+    // The 2*nch stages (pass 1: K of chunk c; pass 2: K and V^T of chunk c)
+    // are register-prefetched one stage ahead: KIT / VIT 16-byte pieces per
+    // thread and plane.
+    constexpr int KIT = NK * (D / 8) / 256, VIT = D * (NK / 8) / 256;
+    uint4 pkh[KIT], pkl[KIT];
+    half8 pvh[VIT], pvl[VIT];
+    auto fetch = [&](int c, bool with_v) {
         const int kbase = c * NK;
-        for (int idx = tid; idx < NK * (D / 8); idx += 256) {
-            const int key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
-            uint4 kh = {0u, 0u, 0u, 0u}, kl = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < KIT; i++) {
+            const int idx = tid + 256 * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
+            pkh[i] = pkl[i] = uint4{0u, 0u, 0u, 0u};
             if (kbase + key < n) {
                 const int64_t off = (int64_t)(beg + kbase + key) * E2 + E + h * D + col;
-                kh = *(const uint4 *)(a.qk_hi + off);
-                kl = *(const uint4 *)(a.qk_lo + off);
+                pkh[i] = *(const uint4 *)(a.qk_hi + off);
+                pkl[i] = *(const uint4 *)(a.qk_lo + off);
             }
-            *(uint4 *)&Kh[key * KST + col] = kh;
-            *(uint4 *)&Kl[key * KST + col] = kl;
         }
         if (!with_v) return;
-        for (int idx = tid; idx < D * (NK / 8); idx += 256) {
-            const int d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+#pragma unroll
+        for (int i = 0; i < VIT; i++) {
+            const int idx = tid + 256 * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
             const int64_t off = (int64_t)(h * D + d) * a.ldv + beg + kbase + k8;
-            half8 vh = {}, vl = {};
+            pvh[i] = pvl[i] = half8{};
             if (kbase + k8 + 8 <= n && v_aligned) {
-                vh = *(const half8 *)(a.vt_hi + off);
-                vl = *(const half8 *)(a.vt_lo + off);
+                pvh[i] = *(const half8 *)(a.vt_hi + off);
+                pvl[i] = *(const half8 *)(a.vt_lo + off);
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; j++)
                     if (kbase + k8 + j < n) {
-                        vh[j] = ((const _Float16 *)a.vt_hi)[off + j];
-                        vl[j] = ((const _Float16 *)a.vt_lo)[off + j];
+                        pvh[i][j] = ((const _Float16 *)a.vt_hi)[off + j];
+                        pvl[i][j] = ((const _Float16 *)a.vt_lo)[off + j];
                     }
             }
+        }
+    };
+    auto commit = [&](bool with_v) {
+#pragma unroll
+        for (int i = 0; i < KIT; i++) {
+            const int idx = tid + 256 * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
+            *(uint4 *)&Kh[key * KST + col] = pkh[i];
+            *(uint4 *)&Kl[key * KST + col] = pkl[i];
+        }
+        if (!with_v) return;
+#pragma unroll
+        for (int i = 0; i < VIT; i++) {
+            const int idx = tid + 256 * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+            const half8 vh = pvh[i], vl = pvl[i];
             *(half4v *)&Vh[d * VST + k8] = half4v{vh[0], vh[1], vh[2], vh[3]};
             *(half4v *)&Vh[d * VST + k8 + 4] = half4v{vh[4], vh[5], vh[6], vh[7]};
             *(half4v *)&Vl[d * VST + k8] = half4v{vl[0], vl[1], vl[2], vl[3]};
@@ -1160,46 +1180,37 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
     };
     const int nch = (n + NK - 1) / NK;
     float mx = -INFINITY;
-    for (int c = 0; c < nch; c++) {  // pass 1: maxima
-        __syncthreads();
-        stage(c, false);
-        __syncthreads();
-        if (active) {
-#pragma unroll
-            for (int kt = 0; kt < NK / 32; kt++) {
-                const int k0 = c * NK + 32 * kt;
-                if (k0 < n) {
-                    const float16v S = scores(k0, 32 * kt);
-#pragma unroll
-                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
-                }
-            }
-        }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
     double sum = 0.0;
     float16v o[D / 32];
 #pragma unroll
     for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
-    for (int c = 0; c < nch; c++) {  // pass 2: p, sum, P.V
+    fetch(0, false);
+    for (int st = 0; st < 2 * nch; st++) {
+        const bool p2 = st >= nch;
+        const int c = p2 ? st - nch : st;
+        __syncthreads();  // the previous stage's LDS reads are done
+        commit(p2);
         __syncthreads();
-        stage(c, true);
-        __syncthreads();
-        if (active) {
+        if (st + 1 < 2 * nch) fetch(st + 1 < nch ? st + 1 : st + 1 - nch, st + 1 >= nch);
+        if (st == nch) mx = fmaxf(mx, __shfl_xor(mx, 32));  // pass 1 complete
+        if (!active) continue;
 #pragma unroll
-            for (int kt = 0; kt < NK / 32; kt++) {
-                const int k0 = c * NK + 32 * kt;
-                if (k0 < n) {
-                    float16v S = scores(k0, 32 * kt);
+        for (int kt = 0; kt < NK / 32; kt++) {
+            const int k0 = c * NK + 32 * kt;
+            if (k0 >= n) continue;
+            float16v S = scores(k0, 32 * kt);
+            if (!p2) {  // pass 1: maxima
 #pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const uint32_t hm = f2h(S[j] - mx) & 0x7fffu;  // s - max <= 0; -inf -> 0
-                        const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
-                        S[j] = p;
-                        sum += (double)p;
-                    }
-                    attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
+                for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
+            } else {    // pass 2: p, sum, P.V
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const uint32_t hm = f2h(S[j] - mx) & 0x7fffu;  // s - max <= 0; -inf -> 0
+                    const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
+                    S[j] = p;
+                    sum += (double)p;
                 }
+                attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
             }
         }
     }
