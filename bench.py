@@ -85,6 +85,7 @@ def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
         "gemm_up_gelu": 2.0 * M * E * I,
         "gemm_down_ln": 2.0 * M * I * E,
         "attention": 4.0 * B * N * N * E,
+        "qkv_attention": 2.0 * M * E * 3 * E + 4.0 * B * N * N * E,
     }.get(name, 0.0)
 
 
@@ -100,6 +101,7 @@ def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
         "gemm_up_gelu": M * E * act + E * I * wb + M * I * act,
         "gemm_down_ln": M * I * act + E * I * wb + 2 * M * E * 4 + M * E * act,
         "attention": M * 3 * E * 4 + M * E * act,
+        "qkv_attention": M * E * act + 3 * E * E * wb + M * E * act,
         "embed_ln": M * 4 + M * E * (4 + act) + M * E * 3 * wb,
         "pool_l2": M * E * 4 + B * E * 4,
     }.get(name, 0.0) if L else 0.0
@@ -130,7 +132,7 @@ def pmc_traffic(csv_path: str, kernel_substr: str):
 # name fragments of the dominant kernels' mangled symbols (for PMC CSV lookup)
 KERNEL_SYMBOL = {
     "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "gemm_kernel<2, 1,",
-    "gemm_down_ln": "gemm_kernel<2, 2,", "attention": "attention_short_kernel", "embed_ln": "embed_ln_kernel",
+    "gemm_down_ln": "gemm_kernel<2, 2,", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
     "pool_l2": "pool_l2_kernel",
 }
 

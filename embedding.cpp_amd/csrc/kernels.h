@@ -82,7 +82,11 @@ struct GemmArgs {
     int N = 0;
     const float *bias = nullptr;   // [N]
     // EPI_QKV: y = b + W.x (f32, as ggml), stored split for the attention MFMAs:
-    // Q | K as hi/lo fp16 planes [Mpad][2E], V transposed as hi/lo planes [E][ldv]
+    // Q | K as hi/lo fp16 planes [Mpad][2E], V transposed as hi/lo planes [E][ldv].
+    // The QKV weight rows are head-major (runtime.cpp): feature h*3D + part*D + d
+    // is row d of head h of Q, K or V (part 0, 1, 2), so a 3D-wide column range
+    // holds one head's Q, K and V (qkv_attention_kernel).
+    int head_dim = 0;
     uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16 bits
     int64_t ldv = 0;
     ActPtr out_act;                // EPI_GELU_ACT: [Mpad][N]; EPI_LN: [Mpad][N]
@@ -122,6 +126,10 @@ constexpr int ATT_QB = 64;    // queries per attention workgroup
 hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s);
 hipError_t launch_gemm(int wtype, int epi, int E_or_bn, const GemmArgs &a, int Mpad, hipStream_t s);
 hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs, int max_len, hipStream_t s);
+// QKV GEMM + attention in one kernel (sentences <= 128 tokens, head dim 32);
+// g: the QKV GemmArgs (head-major weights), a: the AttnArgs (its Q/K/V pointers unused)
+bool qkv_attention_supported(int wtype, int E, int H, int max_len);
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s);
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s);
 hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const float *b, float eps,
                      const ActPtr &out, hipStream_t s);

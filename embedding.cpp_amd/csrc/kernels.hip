@@ -542,12 +542,14 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
     return f;
 }
 
-template <int WT, int EPI, int BN, int NW, int BM>
-__global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtiles, int n_ntiles) {
+// GEMM main loop, shared by gemm_kernel and qkv_attention_kernel:
+// acc[rt][nt] += A[m0 + 16 rt .. ][:] . W[16 (ntile0 + nt) .. ][:]^T for this
+// wave's NTW n-tiles over the whole K (rows m0 .. m0 + BM of A; the A chunks
+// go through `smem`, 2 * A_BUF bytes; returns after a final barrier).
+template <int WT, int NW, int BM, int NTW>
+__device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, int64_t ntile0, char *smem,
+                                              float4v (&acc)[BM / 16][NTW]) {
     constexpr int NT = NW * 64;
-    constexpr int WN = BN / NW;
-    constexpr int NTW = WN / 16;
-    constexpr int NP = NTW / 2;  // column pairs per wave
     constexpr int RT = BM / 16;
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
     constexpr bool F32P = (WT == W_F32);
@@ -555,37 +557,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
-    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
-    constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
-    static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
-    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
-    __shared__ __attribute__((aligned(16))) char smem[SMEM];
-#ifndef GELU_LDS_TABLE
-#define GELU_LDS_TABLE 1
-#endif
-    constexpr bool GT_LDS = GELU_LDS_TABLE && EPI == EPI_GELU_ACT;
-    __shared__ __attribute__((aligned(16))) uint16_t gtab[GT_LDS ? HALF_TABLE_LDS : 8];
-
-    // XCD-aware tile order: linear block ids are dealt round-robin over the 8
-    // XCDs; remap so that each XCD walks a contiguous range, n fastest, so the
-    // N-tiles that share an A panel run on one XCD (bijective for any count).
-    const int nwg = n_mtiles * n_ntiles, orig = blockIdx.x;
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int mt = lin / n_ntiles, ntile = lin - mt * n_ntiles;
-
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int g = lane >> 4, c16 = lane & 15;
-    const int64_t m0 = (int64_t)mt * BM;
-    const int n0 = ntile * BN;
     const int K = args.K, nkc = K / KC, nkb = K >> 5;
-    const int64_t ntile0 = (n0 + wv * WN) >> 4;
     const float unscale = args.W.unscale;
-    if constexpr (GT_LDS) {  // GELU table -> LDS (read after the main loop's barriers)
-        for (int i = tid; i < args.gelu.n_pad / 8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.compact)[i];
-    }
-
-    float4v acc[RT][NTW];
 #pragma unroll
     for (int i = 0; i < RT; i++)
 #pragma unroll
@@ -716,6 +691,52 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         __syncthreads();
     }
 
+}
+
+template <int WT, int EPI, int BN, int NW, int BM>
+__global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtiles, int n_ntiles) {
+    constexpr int NT = NW * 64;
+    constexpr int WN = BN / NW;
+    constexpr int NTW = WN / 16;
+    constexpr int NP = NTW / 2;  // column pairs per wave
+    constexpr int RT = BM / 16;
+    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr bool F32P = (WT == W_F32);
+    constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
+    constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
+    constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
+    constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
+    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
+    constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
+    static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
+    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+#ifndef GELU_LDS_TABLE
+#define GELU_LDS_TABLE 1
+#endif
+    constexpr bool GT_LDS = GELU_LDS_TABLE && EPI == EPI_GELU_ACT;
+    __shared__ __attribute__((aligned(16))) uint16_t gtab[GT_LDS ? HALF_TABLE_LDS : 8];
+
+    // XCD-aware tile order: linear block ids are dealt round-robin over the 8
+    // XCDs; remap so that each XCD walks a contiguous range, n fastest, so the
+    // N-tiles that share an A panel run on one XCD (bijective for any count).
+    const int nwg = n_mtiles * n_ntiles, orig = blockIdx.x;
+    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int mt = lin / n_ntiles, ntile = lin - mt * n_ntiles;
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int g = lane >> 4, c16 = lane & 15;
+    const int64_t m0 = (int64_t)mt * BM;
+    const int n0 = ntile * BN;
+    const int64_t ntile0 = (n0 + wv * WN) >> 4;
+    if constexpr (GT_LDS) {  // GELU table -> LDS (read after the main loop's barriers)
+        for (int i = tid; i < args.gelu.n_pad / 8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.compact)[i];
+    }
+
+    float4v acc[RT][NTW];
+    gemm_mainloop<WT, NW, BM, NTW>(args, m0, ntile0, smem, acc);
+
     // ---- epilogue, in registers.  Lane (g, c16), pair p, row-tile rt, i:
     //      row = m0 + rt*16 + 4g + i, columns col0 + {0, 1} with
     //      col0 = n0 + wv*WN + 32p + 2*c16; values acc[rt][2p][i], acc[rt][2p+1][i].
@@ -744,12 +765,14 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     } else if constexpr (EPI == EPI_QKV) {
         // y = b + W.x in f32 (ggml), split hi = fp16(y), lo = fp16(y - hi) for the
         // attention MFMAs.  A column pair lies wholly in Q|K or in V (E % 32 == 0).
-        const int E = args.N / 3;
+        const int E = args.N / 3, D = args.head_dim;
 #pragma unroll
         for (int p = 0; p < NP; p++) {
-            const int col = colw + 32 * p;
-            const float2v b = *(const float2v *)(args.bias + col);
-            if (col < 2 * E) {
+            const int fcol = colw + 32 * p;  // head-major feature: h*3D + part*D + d (D % 32 == 0)
+            const float2v b = *(const float2v *)(args.bias + fcol);
+            const int hd = fcol / (3 * D), part = (fcol - hd * 3 * D) / D, dd = fcol - hd * 3 * D - part * D;
+            const int col = part * E + hd * D + dd;  // Q | K | V column of the classic layout
+            if (part < 2) {
 #pragma unroll
                 for (int rt = 0; rt < RT; rt++)
 #pragma unroll
@@ -1075,6 +1098,151 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
             if (kt < nkt) attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S[kt]);
         attn_store_ctx<WT, D>(a, o, rs, beg + q0 + r, q0 + r < n, h, hh);
     }
+}
+
+// QKV projection fused with attention, for batches whose sentences all have
+// n <= 128 tokens and heads of D = 32 (MiniLM): one 12-wave workgroup per
+// sentence, so Q, K and V (hi/lo, 4 bytes a value) never leave the CU —
+// the unfused pair writes and re-reads 12 bytes per token and feature.
+// Heads go two at a time: the GEMM main loop (gemm_mainloop, the 128 rows
+// from the sentence's first token) computes the pair's 192 head-major QKV
+// features (kernels.h GemmArgs), one 16-feature n-tile per wave; b + W.x is
+// split hi/lo into the two heads' attention tiles in LDS, and the 8
+// (head, 32-query) attention tasks run as in attention_short_kernel.
+constexpr int QKVA_NW = 12, QKVA_D = 32;  // waves, head dim
+
+template <int WT>
+__global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
+    constexpr int D = QKVA_D, NW = QKVA_NW, BM = 128, NTW = 1, RT = BM / 16;
+    constexpr int NK = 128, KST = D + 8, VST = NK + 4;
+    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr int A_BUF = (WT == W_F32 ? BM * LDA_F * 4 : BM * LDA_H * 2) + (QP ? KB * BM * 4 : 0);
+    constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
+    constexpr int SMEM = (2 * A_BUF > 2 * SLOT) ? 2 * A_BUF : 2 * SLOT;
+    static_assert(NW * 16 == 2 * 3 * D, "one 16-feature n-tile per wave covers a head pair");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
+    const int s = blockIdx.x;
+    const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
+    if (n > NK || n <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int gq = lane >> 4, c16 = lane & 15, r = lane & 31, hh = lane >> 5;
+    const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
+    for (int i = tid; i < a.expt.n_pad / 8; i += NW * 64) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
+    auto slot = [&](int hs, int plane) -> _Float16 * {  // plane: 0 Qh 1 Ql 2 Kh 3 Kl 4 Vh 5 Vl
+        char *base = smem + hs * SLOT;
+        return (_Float16 *)(plane < 4 ? base + plane * NK * KST * 2 : base + 4 * NK * KST * 2 + (plane - 4) * D * VST * 2);
+    };
+    int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
+    asm volatile("" : "+v"(lim));
+    // wave w: n-tile w of the pair = features 32 (w / 2) + 2 c16 + (w % 2) of the
+    // pair's range (the repack's column interleave), i.e. head slot (w / 2) / 3,
+    // part (w / 2) % 3, head dimension 2 c16 + (w % 2)
+    const int blk32 = wv >> 1, hs_w = blk32 / 3, part_w = blk32 % 3, d_w = 2 * c16 + (wv & 1);
+
+    for (int pr = 0; pr < a.H / 2; pr++) {
+        const int fpair = pr * 6 * D;  // first head-major feature of the pair
+        float4v acc[RT][NTW];
+        gemm_mainloop<WT, NW, BM, NTW>(g, beg, (fpair >> 4) + wv, smem, acc);  // ends with a barrier
+        {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values)
+            const float b = g.bias[fpair + 32 * blk32 + 2 * c16 + (wv & 1)];
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++) {
+                half4v hv, lv;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int row = rt * 16 + 4 * gq + i;
+                    const float y = row < n ? b + acc[rt][0][i] : 0.f;
+                    hv[i] = (_Float16)y;
+                    lv[i] = (_Float16)(y - (float)hv[i]);
+                }
+                if (part_w == 2) {
+                    *(half4v *)(slot(hs_w, 4) + d_w * VST + rt * 16 + 4 * gq) = hv;
+                    *(half4v *)(slot(hs_w, 5) + d_w * VST + rt * 16 + 4 * gq) = lv;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int row = rt * 16 + 4 * gq + i;
+                        slot(hs_w, 2 * part_w)[row * KST + d_w] = hv[i];
+                        slot(hs_w, 2 * part_w + 1)[row * KST + d_w] = lv[i];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (wv < 8) {  // attention task (head slot, 32 queries)
+            const int hs = wv >> 2, q0 = (wv & 3) * 32, head = 2 * pr + hs;
+            if (q0 < n) {
+                const _Float16 *Qh = slot(hs, 0), *Ql = slot(hs, 1), *Kh = slot(hs, 2), *Kl = slot(hs, 3);
+                const _Float16 *Vh = slot(hs, 4), *Vl = slot(hs, 5);
+                half8 qh[D / 16], ql[D / 16];
+#pragma unroll
+                for (int ks = 0; ks < D / 16; ks++) {
+                    qh[ks] = *(const half8 *)(Qh + (q0 + r) * KST + 16 * ks + 8 * hh);
+                    ql[ks] = *(const half8 *)(Ql + (q0 + r) * KST + 16 * ks + 8 * hh);
+                }
+                // two passes over the key tiles (the second recomputes the identical
+                // scores): only one 32-key score tile is live, which keeps this
+                // phase inside the 12-wave register budget next to the GEMM's
+                const int nkt = (n + 31) >> 5;
+                auto scores = [&](int kt) {
+                    float16v S = attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql);
+#pragma unroll
+                    for (int j = 0; j < 16; j++) S[j] = S[j] * a.scale;  // ggml_scale after K.Q
+                    if (32 * kt + 32 > n) {
+#pragma unroll
+                        for (int j = 0; j < 16; j++)
+                            if (32 * kt + (j & 3) + 8 * (j >> 2) >= lim) S[j] = -INFINITY;
+                    }
+                    return S;
+                };
+                float mx = -INFINITY;
+                for (int kt = 0; kt < nkt; kt++) {
+                    const float16v S = scores(kt);
+#pragma unroll
+                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
+                }
+                mx = fmaxf(mx, __shfl_xor(mx, 32));
+                double sum = 0.0;
+                float16v o[D / 32];
+#pragma unroll
+                for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
+                for (int kt = 0; kt < nkt; kt++) {
+                    float16v S = scores(kt);
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        const uint32_t hm = f2h(S[j] - mx) & 0x7fffu;  // s - max <= 0; -inf -> 0
+                        const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
+                        S[j] = p;
+                        sum += (double)p;
+                    }
+                    attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
+                }
+                sum += __shfl_xor(sum, 32);
+                attn_store_ctx<WT, D>(a, o, (float)(1.0 / sum), beg + q0 + r, q0 + r < n, head, hh);
+            }
+        }
+        __syncthreads();  // the next pair's A chunks overwrite the attention tiles
+    }
+}
+
+template <int WT>
+static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
+    hipLaunchKernelGGL((qkv_attention_kernel<WT>), dim3(n_seqs), dim3(QKVA_NW * 64), 0, s, g, a);
+    return hipGetLastError();
+}
+
+bool qkv_attention_supported(int wtype, int E, int H, int max_len) {
+    return max_len <= 128 && E / H == QKVA_D && H % 2 == 0 && E % KC == 0 && wtype != W_F32;
+}
+
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
+    switch (wtype) {
+        case W_F16: return qkv_attn_t<W_F16>(g, a, n_seqs, s);
+        case W_Q4_0: return qkv_attn_t<W_Q4_0>(g, a, n_seqs, s);
+        case W_Q4_1: return qkv_attn_t<W_Q4_1>(g, a, n_seqs, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 // Attention for 128 < n <= 512: one workgroup per (128-query block, head,

@@ -333,10 +333,17 @@ std::vector<const uint8_t *> rows_of(const GGUFTensor *t) {
 size_t act_elem_bytes(int wtype) { return wtype == W_F32 ? 4 : wtype == W_F16 ? 2 : 1; }
 size_t act_scale_bytes(int wtype) { return wtype == W_Q4_0 ? 2 : wtype == W_Q4_1 ? 4 : 0; }
 
+// Activation buffers carry GEMM_BM spare rows: qkv_attention_kernel reads the
+// 128-row tile starting at each sentence's first token (rows past M are
+// zero-filled and masked).
 bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, int64_t K) {
+    rows += GEMM_BM;
     if (!dmalloc(track, &a.q, (size_t)rows * K * act_elem_bytes(wtype))) return false;
-    if (act_scale_bytes(wtype) && !dmalloc(track, &a.d, (size_t)rows * (K / 32) * act_scale_bytes(wtype)))
-        return false;
+    HIP_OK(hipMemset(a.q, 0, (size_t)rows * K * act_elem_bytes(wtype)));
+    if (act_scale_bytes(wtype)) {
+        if (!dmalloc(track, &a.d, (size_t)rows * (K / 32) * act_scale_bytes(wtype))) return false;
+        HIP_OK(hipMemset(a.d, 0, (size_t)rows * (K / 32) * act_scale_bytes(wtype)));
+    }
     return true;
 }
 
@@ -424,6 +431,10 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     Workspace &w = R.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
     const bool ln_fused = gemm_ln_fused(wt, E);
+    // QKV + attention in one kernel when every sentence fits one 128-row tile
+    // (env BERT_AMD_UNFUSED=1 forces the two-kernel path, for A/B checks)
+    static const bool force_unfused = std::getenv("BERT_AMD_UNFUSED") != nullptr;
+    const bool fused_qkv_attn = !force_unfused && qkv_attention_supported(wt, E, H, max_len);
 
     EmbedArgs ea;
     ea.tokens = d_tok;
@@ -454,13 +465,12 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         q.W = L.qkv;
         q.N = 3 * E;
         q.bias = L.b_qkv;
+        q.head_dim = D;
         q.qk_hi = w.qk_hi;
         q.qk_lo = w.qk_lo;
         q.vt_hi = w.vt_hi;
         q.vt_lo = w.vt_lo;
         q.ldv = w.cap_rows;
-        LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)Mpad, st));
-
         AttnArgs aa;
         aa.qk_hi = w.qk_hi;
         aa.qk_lo = w.qk_lo;
@@ -473,7 +483,12 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         aa.scale = 1.0f / sqrtf((float)D);
         aa.expt = half_table(R.exp_tab, R.exp_compact, tables().exp_c);
         aa.ctx = w.Ca;
-        LAUNCH_OK("attention", launch_attention(wt, D, aa, n_seqs, max_len, st));
+        if (fused_qkv_attn) {
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, q, aa, n_seqs, st));
+        } else {
+            LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)Mpad, st));
+            LAUNCH_OK("attention", launch_attention(wt, D, aa, n_seqs, max_len, st));
+        }
 
         GemmArgs o;
         o.A = w.Ca;
@@ -581,17 +596,24 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
     const uint32_t wt = hm.layers[0].q_w->type;
     for (const auto &l : hm.layers) {
         DevLayer dl;
-        std::vector<const uint8_t *> rows = rows_of(l.q_w), rk = rows_of(l.k_w), rv = rows_of(l.v_w);
-        rows.insert(rows.end(), rk.begin(), rk.end());
-        rows.insert(rows.end(), rv.begin(), rv.end());
+        // QKV rows head-major (kernels.h GemmArgs EPI_QKV): feature h*3D + part*D + d
+        // <- row d of head h of Q (part 0), K (1) or V (2)
+        const int64_t Dh = E / ctx->hp.n_head;
+        const std::vector<const uint8_t *> rq = rows_of(l.q_w), rk = rows_of(l.k_w), rv = rows_of(l.v_w);
+        std::vector<const uint8_t *> rows((size_t)(3 * E));
+        std::vector<float> bqkv((size_t)3 * E);
+        for (int64_t hd = 0; hd < ctx->hp.n_head; hd++)
+            for (int part = 0; part < 3; part++)
+                for (int64_t d = 0; d < Dh; d++) {
+                    const size_t dst = (size_t)(hd * 3 * Dh + part * Dh + d), src = (size_t)(hd * Dh + d);
+                    rows[dst] = (part == 0 ? rq : part == 1 ? rk : rv)[src];
+                    const GGUFTensor *bt = part == 0 ? l.q_b : part == 1 ? l.k_b : l.v_b;
+                    bqkv[dst] = ((const float *)bt->data)[src];
+                }
         if (!upload_packed(tr, dl.qkv, repack(wt, rows, E)) || !upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E)) ||
             !upload_packed(tr, dl.up, repack(wt, rows_of(l.i_w), E)) ||
             !upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I)))
             return false;
-        std::vector<float> bqkv((size_t)3 * E);
-        std::memcpy(bqkv.data(), l.q_b->data, E * 4);
-        std::memcpy(bqkv.data() + E, l.k_b->data, E * 4);
-        std::memcpy(bqkv.data() + 2 * E, l.v_b->data, E * 4);
         if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
             !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||
             !upload(tr, &dl.ln1_w, l.ln1_w->data, E * 4) || !upload(tr, &dl.ln1_b, l.ln1_b->data, E * 4) ||

@@ -101,6 +101,15 @@ int main(int argc, char **argv) {
     const bool all = !strcmp(which, "all");
     if (all || !strcmp(which, "none")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("qkv  NONE <384,12,128>", q, M, iters);
     if (all || !strcmp(which, "none")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
+    if (all || !strcmp(which, "wg")) {
+        run<W_Q4_0, EPI_QKV, 384, 12, 128>("qkv  <384,12,128>", q, M, iters);
+        run<W_Q4_0, EPI_QKV, 192, 6, 128>("qkv  <192,6,128>", q, M, iters);
+        run<W_Q4_0, EPI_QKV, 128, 4, 128>("qkv  <128,4,128>", q, M, iters);
+        run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   <384,12,128>", u, M, iters);
+        run<W_Q4_0, EPI_GELU_ACT, 192, 6, 128>("up   <192,6,128>", u, M, iters);
+        run<W_Q4_0, EPI_NONE, 384, 12, 128>("qkv NONE <384,12,128>", q, M, iters);
+        run<W_Q4_0, EPI_NONE, 192, 6, 128>("qkv NONE <192,6,128>", q, M, iters);
+    }
     if (all || !strcmp(which, "f16")) {
         // e5-base shapes on F16 weights (C4): E = 768, I = 3072
         GemmArgs q2 = g; q2.K = 768; q2.N = 2304;
