@@ -73,6 +73,7 @@ struct HalfTable {
     int pos_n = 0, neg_n = 0, n_pad = 0;
     int pos_identity = 0;
     uint32_t neg_const = 0;
+    int cap = 0;  // GELU pair view: compact holds (cap + 1) x {table[m], table[0x8000 | m]}
 };
 
 struct GemmArgs {

@@ -122,18 +122,16 @@ __device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, i
     }
 }
 
-// ggml's fp16 GELU table through its LDS-resident compact part (kernels.h
-// HalfTable): finite h below the identity run and above the constant run read
-// LDS; the host verified every other finite entry is h itself (x >= pos_n) or
-// neg_const (compact[pos_n + neg_n]).  Branch-free; non-finite inputs (which
-// b + W.x with finite weights cannot produce) follow their sign's rule instead
-// of ggml's NaN.
-__device__ __forceinline__ uint32_t gelu_lookup(const uint16_t *lds, int pos_n, int neg_n, uint32_t h) {
-    const uint32_t mag = h & 0x7fffu;
-    const bool neg = h > 0x7fffu;
-    const uint32_t idx = neg ? (uint32_t)pos_n + min(mag, (uint32_t)neg_n) : min(mag, (uint32_t)pos_n);
-    const uint32_t v = lds[idx];
-    return (h - (uint32_t)pos_n < 0x8000u - (uint32_t)pos_n) ? h : v;  // positive, >= pos_n: identity
+// ggml's fp16 GELU table through its LDS-resident pair view (kernels.h
+// HalfTable): entry m < cap + 1 holds table[m] (low half) and table[0x8000 | m]
+// (high half); the host verified every finite pattern: negative magnitudes
+// beyond cap read entry cap (ggml's constant run), positive ones beyond cap are
+// h itself (identity run).  Branch-free: and, min, read, shift, select.
+// Non-finite inputs (which b + W.x with finite weights cannot produce) follow
+// their sign's rule instead of ggml's NaN.
+__device__ __forceinline__ uint32_t gelu_lookup(const uint32_t *pair, uint32_t cap, uint32_t h) {
+    const uint32_t v = pair[min(h & 0x7fffu, cap)] >> ((h >> 11) & 16u);
+    return (h - (cap + 1u) < 0x8000u - (cap + 1u)) ? h : v;  // low 16 bits are the result
 }
 
 // ---------------------------------------------------------------------------
@@ -141,83 +139,114 @@ __device__ __forceinline__ uint32_t gelu_lookup(const uint16_t *lds, int pos_n, 
 // task t -> quarter qq = t & 3, block b, row r.  v = (bias + acc) + x; two-pass
 // statistics in double (ggml_norm), combined quarter -> block (two shuffles)
 // -> row (fixed block order); then y = w * (v * scale) + b, stored to X and in
-// the next matmul's activation format.
-template <int WT, int NBLK>
-__device__ void ln_row_phase_q(float *stage, int ld, double *red, int64_t row0, const float *__restrict__ bias,
-                               float *X, const float *__restrict__ lnw, const float *__restrict__ lnb, float eps,
-                               const ActPtr &out, int tid, int nthreads) {
-    constexpr int ncols = NBLK * 32, ntask = 64 * NBLK;
+// the next matmul's activation format.  The caller keeps each task's bias in
+// registers across slices and loads the residual x one slice ahead, so the
+// row phases do not wait on HBM latency.
+struct LnTask {
+    int r, b, qq, c;
+    float4v bias[2];
+};
+
+template <int NBLK, int NT>
+__device__ __forceinline__ void ln_tasks(LnTask (&tk)[64 * NBLK / NT], int tid, const float *__restrict__ bias) {
+#pragma unroll
+    for (int k = 0; k < 64 * NBLK / NT; k++) {
+        const int t = tid + k * NT;
+        tk[k].qq = t & 3;
+        tk[k].b = (t >> 2) % NBLK;
+        tk[k].r = (t >> 2) / NBLK;
+        tk[k].c = 32 * tk[k].b + 8 * tk[k].qq;
+#pragma unroll
+        for (int h = 0; h < 2; h++) tk[k].bias[h] = *(const float4v *)(bias + tk[k].c + 4 * h);
+    }
+}
+
+template <int NBLK, int NT>
+__device__ __forceinline__ void ln_xload(float4v (&xv)[64 * NBLK / NT][2], const LnTask (&tk)[64 * NBLK / NT],
+                                         const float *X, int64_t row0) {
+#pragma unroll
+    for (int k = 0; k < 64 * NBLK / NT; k++) {
+        const float4v *xp = (const float4v *)(X + (row0 + tk[k].r) * (int64_t)(NBLK * 32) + tk[k].c);
+        xv[k][0] = xp[0];
+        xv[k][1] = xp[1];
+    }
+}
+
+template <int WT, int NBLK, int NT>
+__device__ __forceinline__ void ln_row_phase_q(float *stage, int ld, double *red, int64_t row0,
+                                               const LnTask (&tk)[64 * NBLK / NT],
+                                               const float4v (&xv)[64 * NBLK / NT][2], float *X,
+                                               const float *__restrict__ lnw, const float *__restrict__ lnb,
+                                               float eps, const ActPtr &out) {
+    constexpr int ncols = NBLK * 32, TPT = 64 * NBLK / NT;
     double *red1 = red, *red2 = red + 16 * NBLK;
-    for (int t = tid; t < ntask; t += nthreads) {
-        const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
-        float *sp = stage + r * ld + c;
-        const float *xr = X + (row0 + r) * (int64_t)ncols + c;
+#pragma unroll
+    for (int k = 0; k < TPT; k++) {
+        float *sp = stage + tk[k].r * ld + tk[k].c;
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            float4v v = *(float4v *)(sp + 4 * k);
-            const float4v bb = *(const float4v *)(bias + c + 4 * k);
-            const float4v x = *(const float4v *)(xr + 4 * k);
+        for (int h = 0; h < 2; h++) {
+            float4v v = *(float4v *)(sp + 4 * h);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                v[j] = (bb[j] + v[j]) + x[j];
+                v[j] = (tk[k].bias[h][j] + v[j]) + xv[k][h][j];
                 s += (double)v[j];
             }
-            *(float4v *)(sp + 4 * k) = v;
+            *(float4v *)(sp + 4 * h) = v;
         }
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
-        if (qq == 0) red1[r * NBLK + b] = s;
+        if (tk[k].qq == 0) red1[tk[k].r * NBLK + tk[k].b] = s;
     }
     __syncthreads();
-    for (int t = tid; t < ntask; t += nthreads) {
-        const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+#pragma unroll
+    for (int k = 0; k < TPT; k++) {
         double tot = 0.0;
 #pragma unroll
-        for (int k = 0; k < NBLK; k++) tot += red1[r * NBLK + k];
+        for (int q = 0; q < NBLK; q++) tot += red1[tk[k].r * NBLK + q];
         const float mean = (float)(tot / ncols);
-        float *sp = stage + r * ld + c;
+        float *sp = stage + tk[k].r * ld + tk[k].c;
         double s2 = 0.0;
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            float4v v = *(float4v *)(sp + 4 * k);
+        for (int h = 0; h < 2; h++) {
+            float4v v = *(float4v *)(sp + 4 * h);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 v[j] = v[j] - mean;
                 s2 += (double)(v[j] * v[j]);
             }
-            *(float4v *)(sp + 4 * k) = v;
+            *(float4v *)(sp + 4 * h) = v;
         }
         s2 += __shfl_xor(s2, 1);
         s2 += __shfl_xor(s2, 2);
-        if (qq == 0) red2[r * NBLK + b] = s2;
+        if (tk[k].qq == 0) red2[tk[k].r * NBLK + tk[k].b] = s2;
     }
     __syncthreads();
-    for (int t = tid; t < ntask; t += nthreads) {
-        const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+#pragma unroll
+    for (int k = 0; k < TPT; k++) {
         double tot = 0.0;
 #pragma unroll
-        for (int k = 0; k < NBLK; k++) tot += red2[r * NBLK + k];
+        for (int q = 0; q < NBLK; q++) tot += red2[tk[k].r * NBLK + q];
         const float var = (float)(tot / ncols);
         const float scale = 1.0f / sqrtf(var + eps);
-        const float *sp = stage + r * ld + c;
+        const float *sp = stage + tk[k].r * ld + tk[k].c;
         float y[8];
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const float4v v = *(const float4v *)(sp + 4 * k);
-            const float4v w = *(const float4v *)(lnw + c + 4 * k);
-            const float4v bb = *(const float4v *)(lnb + c + 4 * k);
+        for (int h = 0; h < 2; h++) {
+            const float4v v = *(const float4v *)(sp + 4 * h);
+            const float4v w = *(const float4v *)(lnw + tk[k].c + 4 * h);
+            const float4v lb = *(const float4v *)(lnb + tk[k].c + 4 * h);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 float z = v[j] * scale;
                 z = w[j] * z;
-                y[4 * k + j] = z + bb[j];
+                y[4 * h + j] = z + lb[j];
             }
         }
-        float4v *xo = (float4v *)(X + (row0 + r) * (int64_t)ncols + c);
+        float4v *xo = (float4v *)(X + (row0 + tk[k].r) * (int64_t)ncols + tk[k].c);
         xo[0] = float4v{y[0], y[1], y[2], y[3]};
         xo[1] = float4v{y[4], y[5], y[6], y[7]};
-        store_act_quarter<WT>(out, ncols, row0 + r, b, qq, y);
+        store_act_quarter<WT>(out, ncols, row0 + tk[k].r, tk[k].b, tk[k].qq, y);
     }
 }
 
@@ -599,6 +628,26 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
         const char *abuf = smem + (kc & 1) * A_BUF;
 #pragma unroll
         for (int kb = 0; kb < KB; kb++) {
+#ifdef GEMM_NOFOLD  // timing experiment only (wrong results): MFMA chain without the per-block fold
+            if constexpr (QP) {
+                half8 a[RT];
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++)
+                    a[rt] = *(const half8 *)((const _Float16 *)abuf + (rt * 16 + c16) * LDA_H + kb * 32 + 8 * g);
+#pragma unroll
+                for (int nt = 0; nt < NTW; nt++)
+#pragma unroll
+                    for (int rt = 0; rt < RT; rt++) {
+                        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].hi, acc[rt][nt], 0, 0, 0);
+                        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].lo, acc[rt][nt], 0, 0, 0);
+                    }
+                if (kc * KB + kb + 2 < nkb) {
+#pragma unroll
+                    for (int nt = 0; nt < NTW; nt++)
+                        wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
+                }
+            } else
+#endif
             if constexpr (QP) {
                 // Per (row tile, n-tile): blk = A.hi + A.lo  (two MFMAs: the exact
                 // d_w-scaled block dot product, f32-accumulated), then ONE fma
@@ -806,11 +855,28 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         }
     } else {
         // GELU / LayerNorm epilogues through a 16-row LDS slice: one thread per
-        // (32-column block, row).  Row stride BN + 4 floats is odd in 16-byte
-        // slots, so the 16 lanes reading one block of 16 rows hit 16 slots.
-        constexpr int LD = BN + 4, NBLK = BN / 32;
+        // (32-column block quarter, row) task, TPT tasks per thread whose column
+        // operands stay in registers across the slices.  Row stride BN + 4 floats
+        // is odd in 16-byte slots, so the 16 lanes reading one block of 16 rows
+        // hit 16 slots.
+        constexpr int LD = BN + 4, NBLK = BN / 32, TPT = 64 * NBLK / NT;
         float *stage = (float *)smem;
         double *red = (double *)(smem + 16 * LD * 4);  // [2][16][NBLK]
+        constexpr bool LN = EPI == EPI_LN;
+        [[maybe_unused]] LnTask tk[LN ? TPT : 1];
+        [[maybe_unused]] float4v xv[2][LN ? TPT : 1][2];
+        [[maybe_unused]] float4v gb[LN ? 1 : TPT][2];
+        if constexpr (LN) {
+            ln_tasks<NBLK, NT>(tk, tid, args.bias);
+            ln_xload<NBLK, NT>(xv[0], tk, args.X, m0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < TPT; k++) {
+                const int t = tid + k * NT, c = 32 * ((t >> 2) % NBLK) + 8 * (t & 3);
+                gb[k][0] = *(const float4v *)(args.bias + n0 + c);
+                gb[k][1] = *(const float4v *)(args.bias + n0 + c + 4);
+            }
+        }
 #pragma unroll
         for (int rt = 0; rt < RT; rt++) {
             __syncthreads();
@@ -824,22 +890,31 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
             const int64_t row0 = m0 + rt * 16;
             if constexpr (EPI == EPI_GELU_ACT) {
                 // gelu(b + W.x) through ggml's fp16 table, four lanes per block
-                for (int t = tid; t < 64 * NBLK; t += NT) {
+                const uint32_t *tab = (const uint32_t *)(GT_LDS ? gtab : args.gelu.compact);
+                const uint32_t cap = (uint32_t)args.gelu.cap;
+#pragma unroll
+                for (int k = 0; k < TPT; k++) {
+                    const int t = tid + k * NT;
                     const int qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
                     const float *sp = stage + r * LD + c;
                     float y[8];
 #pragma unroll
-                    for (int k = 0; k < 2; k++) {
-                        const float4v v = *(const float4v *)(sp + 4 * k);
-                        const float4v bb = *(const float4v *)(args.bias + n0 + c + 4 * k);
+                    for (int h = 0; h < 2; h++) {
+                        const float4v v = *(const float4v *)(sp + 4 * h);
 #pragma unroll
-                        for (int j = 0; j < 4; j++) y[4 * k + j] = h2f((uint16_t)gelu_lookup(GT_LDS ? gtab : args.gelu.compact, args.gelu.pos_n, args.gelu.neg_n, f2h(bb[j] + v[j])));
+                        for (int j = 0; j < 4; j++)
+#ifdef GELU_IDENTITY_EXPERIMENT  // timing experiment only: skip the table
+                            y[4 * h + j] = gb[k][h][j] + v[j];
+#else
+                            y[4 * h + j] = h2f((uint16_t)gelu_lookup(tab, cap, f2h(gb[k][h][j] + v[j])));
+#endif
                     }
                     store_act_quarter<WT>(args.out_act, args.N, row0 + r, (n0 >> 5) + b, qq, y);
                 }
             } else {
-                ln_row_phase_q<WT, NBLK>(stage, LD, red, row0, args.bias, args.X, args.ln_w, args.ln_b, args.eps,
-                                         args.out_act, tid, NT);
+                if (rt + 1 < RT) ln_xload<NBLK, NT>(xv[(rt + 1) & 1], tk, args.X, row0 + 16);
+                ln_row_phase_q<WT, NBLK, NT>(stage, LD, red, row0, tk, xv[rt & 1], args.X, args.ln_w, args.ln_b, args.eps,
+                                             args.out_act);
             }
         }
     }
@@ -1110,6 +1185,19 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 // split hi/lo into the two heads' attention tiles in LDS, and the 8
 // (head, 32-query) attention tasks run as in attention_short_kernel.
 constexpr int QKVA_NW = 12, QKVA_D = 32;  // waves, head dim
+#ifdef QKVA_PROFILE  // development: per-phase shader-clock totals of thread 0 (tools/gemm_bench qkva)
+__device__ unsigned long long qkva_prof[4];
+#define QKVA_MARK(i)                                                   \
+    do {                                                               \
+        if (tid == 0) {                                                \
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
+            atomicAdd(&qkva_prof[i], (unsigned long long)(t_ - t_last)); \
+            t_last = t_;                                               \
+        }                                                              \
+    } while (0)
+#else
+#define QKVA_MARK(i) do {} while (0)
+#endif
 
 template <int WT>
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
@@ -1139,37 +1227,54 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     // pair's range (the repack's column interleave), i.e. head slot (w / 2) / 3,
     // part (w / 2) % 3, head dimension 2 c16 + (w % 2)
     const int blk32 = wv >> 1, hs_w = blk32 / 3, part_w = blk32 % 3, d_w = 2 * c16 + (wv & 1);
+#ifdef QKVA_PROFILE
+    uint64_t t_last = __builtin_amdgcn_s_memtime();
+#endif
 
     for (int pr = 0; pr < a.H / 2; pr++) {
         const int fpair = pr * 6 * D;  // first head-major feature of the pair
         float4v acc[RT][NTW];
+        QKVA_MARK(0);
         gemm_mainloop<WT, NW, BM, NTW>(g, beg, (fpair >> 4) + wv, smem, acc);  // ends with a barrier
-        {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values)
+        QKVA_MARK(1);
+        {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values).
+            // LDS byte offsets and the row limit are rebuilt per pair behind opaque
+            // moves, so the compiler does not hoist 32 addresses / row masks out of
+            // the pair loop (register pressure: they were spilled to scratch).
             const float b = g.bias[fpair + 32 * blk32 + 2 * c16 + (wv & 1)];
+            int rl = n - 4 * gq;  // rows 4 gq + i of each 16-row tile are valid while rt * 16 + i < rl
+            asm volatile("" : "+v"(rl));
+            if (part_w == 2) {
+                uint32_t off = (uint32_t)((char *)slot(hs_w, 4) - smem) + (uint32_t)(d_w * VST + 4 * gq) * 2;
+                asm volatile("" : "+v"(off));
 #pragma unroll
-            for (int rt = 0; rt < RT; rt++) {
-                half4v hv, lv;
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int row = rt * 16 + 4 * gq + i;
-                    const float y = row < n ? b + acc[rt][0][i] : 0.f;
-                    hv[i] = (_Float16)y;
-                    lv[i] = (_Float16)(y - (float)hv[i]);
-                }
-                if (part_w == 2) {
-                    *(half4v *)(slot(hs_w, 4) + d_w * VST + rt * 16 + 4 * gq) = hv;
-                    *(half4v *)(slot(hs_w, 5) + d_w * VST + rt * 16 + 4 * gq) = lv;
-                } else {
+                for (int rt = 0; rt < RT; rt++) {
+                    half4v hv, lv;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        const int row = rt * 16 + 4 * gq + i;
-                        slot(hs_w, 2 * part_w)[row * KST + d_w] = hv[i];
-                        slot(hs_w, 2 * part_w + 1)[row * KST + d_w] = lv[i];
+                        const float y = rt * 16 + i < rl ? b + acc[rt][0][i] : 0.f;
+                        hv[i] = (_Float16)y;
+                        lv[i] = (_Float16)(y - (float)hv[i]);
                     }
+                    *(half4v *)(smem + off + rt * 32) = hv;
+                    *(half4v *)(smem + off + D * VST * 2 + rt * 32) = lv;
                 }
+            } else {
+                uint32_t off = (uint32_t)((char *)slot(hs_w, 2 * part_w) - smem) + (uint32_t)(4 * gq * KST + d_w) * 2;
+                asm volatile("" : "+v"(off));
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const float y = rt * 16 + i < rl ? b + acc[rt][0][i] : 0.f;
+                        const _Float16 h = (_Float16)y;
+                        *(_Float16 *)(smem + off + (rt * 16 + i) * KST * 2) = h;
+                        *(_Float16 *)(smem + off + NK * KST * 2 + (rt * 16 + i) * KST * 2) = (_Float16)(y - (float)h);
+                    }
             }
         }
         __syncthreads();
+        QKVA_MARK(2);
         if (wv < 8) {  // attention task (head slot, 32 queries)
             const int hs = wv >> 2, q0 = (wv & 3) * 32, head = 2 * pr + hs;
             if (q0 < n) {
@@ -1223,6 +1328,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
             }
         }
         __syncthreads();  // the next pair's A chunks overwrite the attention tiles
+        QKVA_MARK(3);
     }
 }
 

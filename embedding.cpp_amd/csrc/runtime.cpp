@@ -103,8 +103,29 @@ CompactTable compact_table(const std::vector<uint16_t> &full, bool identity_tail
     return c;
 }
 
+// GELU pair view (kernels.hip gelu_lookup): entry m = {table[m], table[0x8000 | m]}
+// for m <= cap = max(pos_n, neg_n); checked on every finite pattern.
+std::vector<uint16_t> pair_table(const std::vector<uint16_t> &full, const CompactTable &c, int &cap) {
+    cap = std::max(c.pos_n, c.neg_n);
+    const int n = 2 * (cap + 1), pad = (n + 7) / 8 * 8;
+    std::vector<uint16_t> t((size_t)pad, 0);
+    for (int m = 0; m <= cap; m++) {
+        t[(size_t)(2 * m)] = full[(size_t)m];
+        t[(size_t)(2 * m + 1)] = full[(size_t)(0x8000 | m)];
+    }
+    for (uint32_t h = 0; h < 65536; h++) {
+        if ((h & 0x7fffu) >= 0x7c00u) continue;
+        const uint32_t m = std::min<uint32_t>(h & 0x7fffu, (uint32_t)cap);
+        uint32_t v = t[2 * m + (h >> 15)];
+        if (h < 0x8000u && h > (uint32_t)cap) v = h;
+        if (v != full[h]) cap = 1 << 20;  // poison: load_impl reports it
+    }
+    return t;
+}
+
 struct HostTables {
-    std::vector<uint16_t> gelu, expt;
+    std::vector<uint16_t> gelu, expt, gelu_pair;
+    int gelu_cap = 0;
     CompactTable gelu_c, exp_c;
     HostTables() : gelu(65536), expt(65536) {
         const float A = 0.044715f, S = 0.79788456080286535587989211986876f;
@@ -115,6 +136,7 @@ struct HostTables {
             expt[i] = f32_to_f16(expf(f));
         }
         gelu_c = compact_table(gelu, true, 0);
+        gelu_pair = pair_table(gelu, gelu_c, gelu_cap);
         exp_c = compact_table(expt, false, 1);  // soft_max only feeds s - max <= 0
     }
 };
@@ -516,6 +538,8 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         u.bias = L.b_up;
         u.out_act = w.Ua;
         u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
+        u.gelu.n_pad = (int)tables().gelu_pair.size();  // the pair view (kernels.hip gelu_lookup)
+        u.gelu.cap = tables().gelu_cap;
         LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)Mpad, st));
 
         GemmArgs dn;
@@ -589,7 +613,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
         !upload(tr, &R.ln_e_b, hm.ln_e_b->data, hm.ln_e_b->nbytes) ||
         !upload(tr, &R.gelu_tab, tables().gelu.data(), 65536 * 2) ||
         !upload(tr, &R.exp_tab, tables().expt.data(), 65536 * 2) ||
-        !upload(tr, &R.gelu_compact, tables().gelu_c.compact.data(), tables().gelu_c.compact.size() * 2) ||
+        !upload(tr, &R.gelu_compact, tables().gelu_pair.data(), tables().gelu_pair.size() * 2) ||
         !upload(tr, &R.exp_compact, tables().exp_c.compact.data(), tables().exp_c.compact.size() * 2))
         return false;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
@@ -761,9 +785,13 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
                 hp.n_intermediate, hp.n_max_tokens);
         return nullptr;
     }
-    if ((int)tables().gelu_c.compact.size() > HALF_TABLE_LDS || (int)tables().exp_c.compact.size() > EXP_TABLE_LDS) {
+    if (tables().gelu_cap >= (1 << 20) || tables().gelu_c.pos_n >= (1 << 20) || tables().exp_c.pos_n >= (1 << 20)) {
+        set_err("fp16 GELU/exp table self-check failed: the device lookup rules do not reproduce this host's tables");
+        return nullptr;
+    }
+    if ((int)tables().gelu_pair.size() > HALF_TABLE_LDS || (int)tables().exp_c.compact.size() > EXP_TABLE_LDS) {
         set_err("this host's libm gives fp16 GELU/exp tables whose compact part exceeds LDS (%zu, %zu entries)",
-                tables().gelu_c.compact.size(), tables().exp_c.compact.size());
+                tables().gelu_pair.size(), tables().exp_c.compact.size());
         return nullptr;
     }
     // devices

@@ -54,7 +54,7 @@ static void run(const char *name, GemmArgs a, int M, int iters) {
 int main(int argc, char **argv) {
     const int M = 131072, E = 384, I = 1536, iters = argc > 1 ? atoi(argv[1]) : 20;
     const int K_max = I, N_max = 3 * I;
-    GemmArgs g;
+    GemmArgs g{};
     {   // activations: sized for the largest K (3072) in the widest format used (fp16); values irrelevant
         void *aq;
         CK(hipMalloc(&aq, (size_t)M * 3072 * 4));
@@ -90,9 +90,11 @@ int main(int argc, char **argv) {
     g.gelu.compact = (const uint16_t *)dev_random(36864 * 2, 6, 1);
     g.gelu.pos_n = 17091;
     g.gelu.neg_n = 17705;
-    g.gelu.n_pad = 34800;
+    g.gelu.n_pad = 35416;
+    g.gelu.cap = 17705;
     g.gelu.pos_identity = 1;
 
+    g.head_dim = 32;  // EPI_QKV's head-major remap (kernels.h GemmArgs)
     GemmArgs q = g; q.K = E; q.N = 3 * E;
     GemmArgs u = g; u.K = E; u.N = I;
     GemmArgs o = g; o.K = E; o.N = E;
@@ -110,9 +112,61 @@ int main(int argc, char **argv) {
         run<W_Q4_0, EPI_NONE, 384, 12, 128>("qkv NONE <384,12,128>", q, M, iters);
         run<W_Q4_0, EPI_NONE, 192, 6, 128>("qkv NONE <192,6,128>", q, M, iters);
     }
+    if (all || !strcmp(which, "epi")) {
+        run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   GELU <384,12,128>", u, M, iters);
+        run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
+        run<W_Q4_0, EPI_LN, 384, 12, 128>("o    LN   <384,12,128>", o, M, iters);
+        run<W_Q4_0, EPI_NONE, 384, 12, 128>("o    NONE <384,12,128>", o, M, iters);
+        run<W_Q4_0, EPI_LN, 384, 12, 128>("down LN   <384,12,128>", d, M, iters);
+        run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
+    }
+#ifdef QKVA_PROFILE
+    if (!strcmp(which, "qkva")) {  // fused QKV + attention, 1024 sentences of 128 tokens
+        const int S = M / 128;
+        std::vector<int32_t> offs(S + 1);
+        for (int i = 0; i <= S; i++) offs[i] = 128 * i;
+        int32_t *doffs;
+        CK(hipMalloc(&doffs, (S + 1) * 4));
+        CK(hipMemcpy(doffs, offs.data(), (S + 1) * 4, hipMemcpyHostToDevice));
+        AttnArgs a{};
+        a.offsets = doffs; a.E = E; a.H = 12; a.scale = 0.1767767f;
+        a.expt.compact = (const uint16_t *)dev_random(EXP_TABLE_LDS * 2, 7, 1);
+        a.expt.pos_n = 1; a.expt.neg_n = 19544; a.expt.n_pad = 19552;
+        a.ctx.q = oq; a.ctx.d = od;
+        GemmArgs qq = q;
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        for (int i = 0; i < 2; i++) CK(launch_qkv_attention(W_Q4_0, qq, a, S, 0));
+        unsigned long long z[4] = {0, 0, 0, 0};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(qkva_prof), z, sizeof z));
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; i++) CK(launch_qkv_attention(W_Q4_0, qq, a, S, 0));
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(qkva_prof), sizeof z));
+        const double tot = (double)z[0] + z[1] + z[2] + z[3];
+        printf("qkv_attention %.1f us/launch; phase shares: pre %.3f gemm %.3f split %.3f attn %.3f (cycles/WG %.0f)\n",
+               ms * 1000.0 / iters, z[0] / tot, z[1] / tot, z[2] / tot, z[3] / tot, tot / iters / S);
+    }
+#endif
+    if (!strcmp(which, "gelu")) {
+        run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   GELU <384,12,128>", u, M, iters);
+        run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
+    }
+    if (all || !strcmp(which, "ln")) {
+        run<W_Q4_0, EPI_LN, 384, 12, 128>("o    LN   <384,12,128>", o, M, iters);
+        run<W_Q4_0, EPI_LN, 384, 6, 64>("o    LN   <384,6,64>", o, M, iters);
+        run<W_Q4_0, EPI_NONE, 384, 6, 64>("o    NONE <384,6,64>", o, M, iters);
+        run<W_Q4_0, EPI_LN, 384, 12, 64>("o    LN   <384,12,64>", o, M, iters);
+        run<W_Q4_0, EPI_LN, 384, 12, 128>("down LN   <384,12,128>", d, M, iters);
+        run<W_Q4_0, EPI_LN, 384, 6, 64>("down LN   <384,6,64>", d, M, iters);
+        run<W_Q4_0, EPI_NONE, 384, 6, 64>("down NONE <384,6,64>", d, M, iters);
+        run<W_Q4_0, EPI_LN, 384, 12, 64>("down LN   <384,12,64>", d, M, iters);
+    }
     if (all || !strcmp(which, "f16")) {
         // e5-base shapes on F16 weights (C4): E = 768, I = 3072
-        GemmArgs q2 = g; q2.K = 768; q2.N = 2304;
+        GemmArgs q2 = g; q2.K = 768; q2.N = 2304; q2.head_dim = 64;
         GemmArgs u2 = g; u2.K = 768; u2.N = 3072;
         GemmArgs d2 = g; d2.K = 3072; d2.N = 768;
         const int M2 = 65536;

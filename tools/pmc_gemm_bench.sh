@@ -4,6 +4,6 @@ export TMPDIR=/tmp
 OUT=$PWD/gpurun_out/pmcgb; mkdir -p $OUT
 for p in "cyc:SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES" "ins:SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM" "lds:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC" "act:SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM" "tcp:TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
   name=${p%%:*}; ctr=${p#*:}
-  ( cd /tmp && timeout -k 10 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/$name -o gb -- $GRAFT_REPO_ROOT/build/gemm_bench 3 none ) > $OUT/$name.log 2>&1
+  ( cd /tmp && timeout -k 10 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/$name -o gb -- $GRAFT_REPO_ROOT/build/gemm_bench 3 ${1:-none} ) > $OUT/$name.log 2>&1
   echo "$name rc=$?"
 done
