@@ -575,9 +575,13 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
 // acc[rt][nt] += A[m0 + 16 rt .. ][:] . W[16 (ntile0 + nt) .. ][:]^T for this
 // wave's NTW n-tiles over the whole K (rows m0 .. m0 + BM of A; the A chunks
 // go through `smem`, 2 * A_BUF bytes; returns after a final barrier).
-template <int WT, int NW, int BM, int NTW>
+// Lane (g, c16) holds acc[rt][nt][i] = C[row 16 rt + 4 g + i][col c16 of the
+// n-tile]; with TRANS (Q4 / F16 only) the MFMA operands are swapped and it
+// holds C[row 16 rt + c16][col 4 g + i] (four adjacent columns of one row).
+template <int WT, int NW, int BM, int NTW, bool TRANS = false>
 __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, int64_t ntile0, char *smem,
                                               float4v (&acc)[BM / 16][NTW]) {
+    static_assert(!TRANS || WT != W_F32, "transposed main loop: fp16 MFMA formats only");
     constexpr int NT = NW * 64;
     constexpr int RT = BM / 16;
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
@@ -657,17 +661,24 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 constexpr int T = RT * NTW;
                 const float *sc = (const float *)(abuf + A_BYTES) + kb * BM;
                 half8 a[RT];
-                float4v da[RT];
+                float4v da[RT];  // TRANS: da[rt][0] = d_a of row 16 rt + c16
                 auto lds_a = [&](int rt) {
                     a[rt] = *(const half8 *)((const _Float16 *)abuf + (rt * 16 + c16) * LDA_H + kb * 32 + 8 * g);
-                    da[rt] = *(const float4v *)(sc + rt * 16 + g * 4);
+                    if constexpr (TRANS)
+                        da[rt][0] = sc[rt * 16 + c16];
+                    else
+                        da[rt] = *(const float4v *)(sc + rt * 16 + g * 4);
+                };
+                auto mfma = [&](const half8 &x, const half8 &w, const float4v &c) {
+                    return TRANS ? __builtin_amdgcn_mfma_f32_16x16x32_f16(w, x, c, 0, 0, 0)
+                                 : __builtin_amdgcn_mfma_f32_16x16x32_f16(x, w, c, 0, 0, 0);
                 };
 #pragma unroll
                 for (int rt = 0; rt < RT; rt++)
                     if (rt * NTW <= 1) lds_a(rt);
                 float4v blk[2];
-                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb & 1][0].hi, zero4, 0, 0, 0);
-                blk[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], wf[kb & 1][0].lo, blk[0], 0, 0, 0);
+                blk[0] = mfma(a[0], wf[kb & 1][0].hi, zero4);
+                blk[0] = mfma(a[0], wf[kb & 1][0].lo, blk[0]);
 #pragma unroll
                 for (int t = 0; t < T; t++) {
 #pragma unroll
@@ -675,16 +686,14 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                         if (rt * NTW == t + 2) lds_a(rt);
                     if (t + 1 < T) {
                         const int rt1 = (t + 1) / NTW, nt1 = (t + 1) % NTW;
-                        blk[(t + 1) & 1] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb & 1][nt1].hi, zero4, 0, 0, 0);
-                        blk[(t + 1) & 1] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt1], wf[kb & 1][nt1].lo, blk[(t + 1) & 1], 0, 0, 0);
+                        blk[(t + 1) & 1] = mfma(a[rt1], wf[kb & 1][nt1].hi, zero4);
+                        blk[(t + 1) & 1] = mfma(a[rt1], wf[kb & 1][nt1].lo, blk[(t + 1) & 1]);
                     }
                     const int rt = t / NTW, nt = t % NTW;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         float v = acc[rt][nt][i];
-                        v = __builtin_fmaf(da[rt][i], blk[t & 1][i], v);
+                        v = __builtin_fmaf(TRANS ? da[rt][0] : da[rt][i], blk[t & 1][i], v);
                         asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
                         acc[rt][nt][i] = v;
                     }
@@ -704,7 +713,8 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 for (int nt = 0; nt < NTW; nt++)
 #pragma unroll
                     for (int rt = 0; rt < RT; rt++)
-                        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].h, acc[rt][nt], 0, 0, 0);
+                        acc[rt][nt] = TRANS ? __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[kb & 1][nt].h, a[rt], acc[rt][nt], 0, 0, 0)
+                                            : __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].h, acc[rt][nt], 0, 0, 0);
                 if (kc * KB + kb + 2 < nkb) {
 #pragma unroll
                     for (int nt = 0; nt < NTW; nt++) wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
@@ -1223,10 +1233,14 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     };
     int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
     asm volatile("" : "+v"(lim));
-    // wave w: n-tile w of the pair = features 32 (w / 2) + 2 c16 + (w % 2) of the
-    // pair's range (the repack's column interleave), i.e. head slot (w / 2) / 3,
-    // part (w / 2) % 3, head dimension 2 c16 + (w % 2)
-    const int blk32 = wv >> 1, hs_w = blk32 / 3, part_w = blk32 % 3, d_w = 2 * c16 + (wv & 1);
+    // wave w: n-tile w of the pair = features 16 w .. 16 w + 15 of the pair's
+    // range (g.W is this kernel's own copy of the head-major QKV weights, in
+    // plain tile order), i.e. head slot w / 6, part (w % 6) / 2, head dims
+    // d0 .. d0 + 15 with d0 = 16 (w % 2).  Q and K waves run the transposed main
+    // loop (a lane holds one row x four adjacent dims: 8-byte stores into the
+    // row-major Q / K tiles), V waves the plain one (one dim x four adjacent
+    // rows: 8-byte stores into V^T).
+    const int hs_w = wv / 6, part_w = (wv % 6) / 2, d0 = 16 * (wv & 1);
 #ifdef QKVA_PROFILE
     uint64_t t_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -1235,17 +1249,20 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
         const int fpair = pr * 6 * D;  // first head-major feature of the pair
         float4v acc[RT][NTW];
         QKVA_MARK(0);
-        gemm_mainloop<WT, NW, BM, NTW>(g, beg, (fpair >> 4) + wv, smem, acc);  // ends with a barrier
+        if (part_w == 2)  // ends with a barrier
+            gemm_mainloop<WT, NW, BM, NTW, false>(g, beg, (fpair >> 4) + wv, smem, acc);
+        else
+            gemm_mainloop<WT, NW, BM, NTW, true>(g, beg, (fpair >> 4) + wv, smem, acc);
         QKVA_MARK(1);
         {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values).
-            // LDS byte offsets and the row limit are rebuilt per pair behind opaque
-            // moves, so the compiler does not hoist 32 addresses / row masks out of
+            // LDS byte offsets and row limits are rebuilt per pair behind opaque
+            // moves, so the compiler does not hoist addresses / row masks out of
             // the pair loop (register pressure: they were spilled to scratch).
-            const float b = g.bias[fpair + 32 * blk32 + 2 * c16 + (wv & 1)];
-            int rl = n - 4 * gq;  // rows 4 gq + i of each 16-row tile are valid while rt * 16 + i < rl
-            asm volatile("" : "+v"(rl));
             if (part_w == 2) {
-                uint32_t off = (uint32_t)((char *)slot(hs_w, 4) - smem) + (uint32_t)(d_w * VST + 4 * gq) * 2;
+                const float b = g.bias[fpair + 16 * wv + c16];
+                int rl = n - 4 * gq;  // row 16 rt + 4 gq + i is valid while 16 rt + i < rl
+                asm volatile("" : "+v"(rl));
+                uint32_t off = (uint32_t)((char *)slot(hs_w, 4) - smem) + (uint32_t)((d0 + c16) * VST + 4 * gq) * 2;
                 asm volatile("" : "+v"(off));
 #pragma unroll
                 for (int rt = 0; rt < RT; rt++) {
@@ -1260,17 +1277,23 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     *(half4v *)(smem + off + D * VST * 2 + rt * 32) = lv;
                 }
             } else {
-                uint32_t off = (uint32_t)((char *)slot(hs_w, 2 * part_w) - smem) + (uint32_t)(4 * gq * KST + d_w) * 2;
+                const float4v b4 = *(const float4v *)(g.bias + fpair + 16 * wv + 4 * gq);
+                int rl = n - c16;  // row 16 rt + c16 is valid while 16 rt < rl
+                asm volatile("" : "+v"(rl));
+                uint32_t off = (uint32_t)((char *)slot(hs_w, 2 * part_w) - smem) + (uint32_t)(c16 * KST + d0 + 4 * gq) * 2;
                 asm volatile("" : "+v"(off));
 #pragma unroll
-                for (int rt = 0; rt < RT; rt++)
+                for (int rt = 0; rt < RT; rt++) {
+                    half4v hv, lv;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        const float y = rt * 16 + i < rl ? b + acc[rt][0][i] : 0.f;
-                        const _Float16 h = (_Float16)y;
-                        *(_Float16 *)(smem + off + (rt * 16 + i) * KST * 2) = h;
-                        *(_Float16 *)(smem + off + NK * KST * 2 + (rt * 16 + i) * KST * 2) = (_Float16)(y - (float)h);
+                        const float y = rt * 16 < rl ? b4[i] + acc[rt][0][i] : 0.f;
+                        hv[i] = (_Float16)y;
+                        lv[i] = (_Float16)(y - (float)hv[i]);
                     }
+                    *(half4v *)(smem + off + rt * 16 * KST * 2) = hv;
+                    *(half4v *)(smem + off + NK * KST * 2 + rt * 16 * KST * 2) = lv;
+                }
             }
         }
         __syncthreads();

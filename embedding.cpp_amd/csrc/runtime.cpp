@@ -167,6 +167,7 @@ struct DevMat {
 
 struct DevLayer {
     WPtr qkv, o, up, down;
+    WPtr qkv_plain;  // head-major QKV in plain tile order: qkv_attention_kernel's copy (when supported)
     float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
 };
@@ -506,7 +507,9 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         aa.expt = half_table(R.exp_tab, R.exp_compact, tables().exp_c);
         aa.ctx = w.Ca;
         if (fused_qkv_attn) {
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, q, aa, n_seqs, st));
+            GemmArgs qf = q;
+            qf.W = L.qkv_plain;
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, n_seqs, st));
         } else {
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)Mpad, st));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, n_seqs, max_len, st));
@@ -634,6 +637,15 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                     const GGUFTensor *bt = part == 0 ? l.q_b : part == 1 ? l.k_b : l.v_b;
                     bqkv[dst] = ((const float *)bt->data)[src];
                 }
+        if (qkv_attention_supported(ctx->wtype, (int)E, (int)ctx->hp.n_head, 128)) {
+            // undo repack's column interleave (row 32p + 2c + t <- 32p + 16t + c) so
+            // that repacked tile j holds features 16j .. 16j + 15 in order
+            std::vector<const uint8_t *> plain(rows.size());
+            for (size_t pr = 0; pr < rows.size() / 32; pr++)
+                for (int t = 0; t < 2; t++)
+                    for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = rows[32 * pr + 16 * t + c];
+            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E))) return false;
+        }
         if (!upload_packed(tr, dl.qkv, repack(wt, rows, E)) || !upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E)) ||
             !upload_packed(tr, dl.up, repack(wt, rows_of(l.i_w), E)) ||
             !upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I)))

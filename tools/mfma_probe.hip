@@ -244,6 +244,9 @@ int main() {
     hipMalloc(&w, wn * 16);
     hipMemset(w, 0, wn * 16);
     for (int wv = 1; wv <= 3; wv++) {
+        run<1, 4>("32x32 no fold (reg only)", wv, out, w);
+        run<3, 4>("32x32 pipelined (reg only)", wv, out, w);
+        run<7, 4>("32x32 pipelined pk fold", wv, out, w);
         run<5, 4>("16x16 pipelined (reg only)", wv, out, w);
         run<8, 4>("16x16 + LDS A/d_a reads", wv, out, w);
         run<9, 4>("16x16 + LDS + W global", wv, out, w);
