@@ -578,9 +578,37 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
 // Lane (g, c16) holds acc[rt][nt][i] = C[row 16 rt + 4 g + i][col c16 of the
 // n-tile]; with TRANS (Q4 / F16 only) the MFMA operands are swapped and it
 // holds C[row 16 rt + c16][col 4 g + i] (four adjacent columns of one row).
+// The loop's first loads (A chunk 0 into registers, W blocks 0 and 1) come
+// from a MainloopPre the caller filled with mainloop_preload, early enough
+// for their latency to hide behind other work where it can.
+template <int WT, int NW, int BM, int NTW>
+struct MainloopPre {
+    static constexpr int IT = (BM * (KC / 16) + NW * 64 - 1) / (NW * 64);
+    AReg ar[IT];
+    WFrag<WT> wf[WT == W_F32 ? 1 : 2][NTW];
+};
+
+template <int WT, int NW, int BM, int NTW>
+__device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW> &pre, const GemmArgs &args, int64_t m0,
+                                                 int64_t ntile0) {
+    constexpr int NT = NW * 64, ITEMS = BM * (KC / 16), IT = MainloopPre<WT, NW, BM, NTW>::IT;
+    const int tid = threadIdx.x, nkb = args.K >> 5;
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+        const int item = tid + it * NT;
+        if (item < ITEMS) a_load<WT>(pre.ar[it], args.A, args.K, m0, 0, item);
+    }
+    if constexpr (WT != W_F32) {
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+            for (int nt = 0; nt < NTW; nt++) pre.wf[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kb);
+    }
+}
+
 template <int WT, int NW, int BM, int NTW, bool TRANS = false>
 __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, int64_t ntile0, char *smem,
-                                              float4v (&acc)[BM / 16][NTW]) {
+                                              float4v (&acc)[BM / 16][NTW], const MainloopPre<WT, NW, BM, NTW> &pre) {
     static_assert(!TRANS || WT != W_F32, "transposed main loop: fp16 MFMA formats only");
     constexpr int NT = NW * 64;
     constexpr int RT = BM / 16;
@@ -603,10 +631,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
 #pragma unroll
     for (int it = 0; it < IT; it++) {
         const int item = tid + it * NT;
-        if (item < ITEMS) {
-            a_load<WT>(ar[it], args.A, K, m0, 0, item);
-            a_store<WT, BM>(ar[it], smem, item, unscale);
-        }
+        if (item < ITEMS) a_store<WT, BM>(pre.ar[it], smem, item, unscale);
     }
     // W fragments of the two blocks in flight: block b lives in wf[b & 1] and
     // is replaced by block b + 2 as soon as its MFMAs are issued
@@ -615,7 +640,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
 #pragma unroll
         for (int kb = 0; kb < 2; kb++)
 #pragma unroll
-            for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kb);
+            for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = pre.wf[kb][nt];
     }
     __syncthreads();
 
@@ -794,7 +819,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     }
 
     float4v acc[RT][NTW];
-    gemm_mainloop<WT, NW, BM, NTW>(args, m0, ntile0, smem, acc);
+    {
+        MainloopPre<WT, NW, BM, NTW> pre;
+        mainloop_preload(pre, args, m0, ntile0);
+        gemm_mainloop<WT, NW, BM, NTW>(args, m0, ntile0, smem, acc, pre);
+    }
 
     // ---- epilogue, in registers.  Lane (g, c16), pair p, row-tile rt, i:
     //      row = m0 + rt*16 + 4g + i, columns col0 + {0, 1} with
@@ -988,6 +1017,26 @@ __device__ __forceinline__ void attn_pv(float16v *o, const _Float16 *Vh, const _
             const half8 vl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[dt], 0, 0, 0);
+        }
+    }
+}
+
+// The same with P given as the table's fp16 values (two 8-key halves).
+template <int D>
+__device__ __forceinline__ void attn_pv_h(float16v *o, const _Float16 *Vh, const _Float16 *Vl, int vst, int k0, int r,
+                                          int hh, const half8 (&ph)[2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+        const int key = k0 + 16 * ks + 4 * hh;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; dt++) {
+            const int off = (dt * 32 + r) * vst + key;
+            const half4v h0 = *(const half4v *)&Vh[off], h1 = *(const half4v *)&Vh[off + 8];
+            const half4v l0 = *(const half4v *)&Vl[off], l1 = *(const half4v *)&Vl[off + 8];
+            const half8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+            const half8 vl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph[ks], o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph[ks], o[dt], 0, 0, 0);
         }
     }
 }
@@ -1249,10 +1298,12 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
         const int fpair = pr * 6 * D;  // first head-major feature of the pair
         float4v acc[RT][NTW];
         QKVA_MARK(0);
+        MainloopPre<WT, NW, BM, NTW> pre;  // (loading it during the previous pair's attention measured no faster)
+        mainloop_preload(pre, g, beg, (fpair >> 4) + wv);
         if (part_w == 2)  // ends with a barrier
-            gemm_mainloop<WT, NW, BM, NTW, false>(g, beg, (fpair >> 4) + wv, smem, acc);
+            gemm_mainloop<WT, NW, BM, NTW, false>(g, beg, (fpair >> 4) + wv, smem, acc, pre);
         else
-            gemm_mainloop<WT, NW, BM, NTW, true>(g, beg, (fpair >> 4) + wv, smem, acc);
+            gemm_mainloop<WT, NW, BM, NTW, true>(g, beg, (fpair >> 4) + wv, smem, acc, pre);
         QKVA_MARK(1);
         {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values).
             // LDS byte offsets and row limits are rebuilt per pair behind opaque
@@ -1298,6 +1349,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
         }
         __syncthreads();
         QKVA_MARK(2);
+
         if (wv < 8) {  // attention task (head slot, 32 queries)
             const int hs = wv >> 2, q0 = (wv & 3) * 32, head = 2 * pr + hs;
             if (q0 < n) {
@@ -1311,12 +1363,13 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                 }
                 // two passes over the key tiles (the second recomputes the identical
                 // scores): only one 32-key score tile is live, which keeps this
-                // phase inside the 12-wave register budget next to the GEMM's
+                // phase inside the 12-wave register budget next to the GEMM's.
+                // Pass 1 takes the max of the unscaled K.Q: x -> fl(x * scale) is
+                // monotonic for scale > 0, so fl(max * scale) is ggml's max of the
+                // scaled scores.
                 const int nkt = (n + 31) >> 5;
                 auto scores = [&](int kt) {
                     float16v S = attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql);
-#pragma unroll
-                    for (int j = 0; j < 16; j++) S[j] = S[j] * a.scale;  // ggml_scale after K.Q
                     if (32 * kt + 32 > n) {
 #pragma unroll
                         for (int j = 0; j < 16; j++)
@@ -1330,21 +1383,23 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 #pragma unroll
                     for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
                 }
-                mx = fmaxf(mx, __shfl_xor(mx, 32));
+                mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
                 double sum = 0.0;
                 float16v o[D / 32];
 #pragma unroll
                 for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
                 for (int kt = 0; kt < nkt; kt++) {
-                    float16v S = scores(kt);
+                    const float16v S = scores(kt);
+                    half8 ph[2];
 #pragma unroll
                     for (int j = 0; j < 16; j++) {
-                        const uint32_t hm = f2h(S[j] - mx) & 0x7fffu;  // s - max <= 0; -inf -> 0
-                        const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
-                        S[j] = p;
-                        sum += (double)p;
+                        // ggml_scale after K.Q, then p = exp_tab[fp16(s - max)] (s - max <= 0; -inf -> 0)
+                        const uint32_t hm = f2h(S[j] * a.scale - mx) & 0x7fffu;
+                        const uint16_t pb = etab[epos + min(hm, (uint32_t)eneg)];
+                        ph[j >> 3][j & 7] = __builtin_bit_cast(_Float16, pb);
+                        sum += (double)h2f(pb);
                     }
-                    attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
+                    attn_pv_h<D>(o, Vh, Vl, VST, 32 * kt, r, hh, ph);
                 }
                 sum += __shfl_xor(sum, 32);
                 attn_store_ctx<WT, D>(a, o, (float)(1.0 / sum), beg + q0 + r, q0 + r < n, head, hh);
