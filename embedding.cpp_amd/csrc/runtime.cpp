@@ -194,6 +194,8 @@ struct ProfEntry {
 struct Replica {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;               // second row group (run_pipeline)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void *word = nullptr, *pos = nullptr, *type = nullptr;
     float *ln_e_w = nullptr, *ln_e_b = nullptr;
     std::vector<DevLayer> L;
@@ -432,9 +434,10 @@ void drain_profile(Replica &R) {
     R.pending.clear();
 }
 
-#define LAUNCH_OK(name, expr)                                                             \
+#define LAUNCH_OK(name, expr) LAUNCH_ON(name, st, expr)
+#define LAUNCH_ON(name, stream, expr)                                                     \
     do {                                                                                  \
-        Launch lp_(R, st, name);                                                          \
+        Launch lp_(R, stream, name);                                                      \
         hipError_t e_ = (expr);                                                           \
         if (e_ != hipSuccess) {                                                           \
             set_err("kernel %s launch failed: %s", name, hipGetErrorString(e_));          \
@@ -442,45 +445,22 @@ void drain_profile(Replica &R) {
         }                                                                                 \
     } while (0)
 
-// The fixed pipeline over a ragged batch already resident on the device.
-bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
-                  int n_seqs, float *d_out, hipStream_t st) {
+// One encoder layer over the row group [row0, row0 + rows) (sentences
+// d_off[0 .. nseq), absolute row offsets).  Xa / Ca / Ua / X point at the
+// group's first row; the QKV + attention kernels index rows absolutely through
+// the offsets, so they get the workspace bases (the unfused pair only runs
+// with one group, row0 == 0).
+bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
+               int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa, ActPtr Ca, ActPtr Ua, float *X,
+               hipStream_t st) {
     const HParams &hp = ctx->hp;
-    const int64_t M = h_off[n_seqs];
-    const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
-    int max_len = 0;
-    for (int s = 0; s < n_seqs; s++) max_len = std::max(max_len, h_off[s + 1] - h_off[s]);
-    if (!ensure_workspace(ctx, R, Mpad, n_seqs)) return false;
     Workspace &w = R.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
-    const bool ln_fused = gemm_ln_fused(wt, E);
-    // QKV + attention in one kernel when every sentence fits one 128-row tile
-    // (env BERT_AMD_UNFUSED=1 forces the two-kernel path, for A/B checks)
-    static const bool force_unfused = std::getenv("BERT_AMD_UNFUSED") != nullptr;
-    const bool fused_qkv_attn = !force_unfused && qkv_attention_supported(wt, E, H, max_len);
-
-    EmbedArgs ea;
-    ea.tokens = d_tok;
-    ea.offsets = d_off;
-    ea.n_seqs = n_seqs;
-    ea.M = (int)M;
-    ea.E = E;
-    ea.n_vocab = hp.n_vocab;
-    ea.n_pos = hp.n_max_tokens;
-    ea.word = R.word;
-    ea.pos = R.pos;
-    ea.type = R.type;
-    ea.word_t = wtype_of(ctx->word_t);
-    ea.pos_t = wtype_of(ctx->pos_t);
-    ea.type_t = wtype_of(ctx->type_t);
-    ea.ln_w = R.ln_e_w;
-    ea.ln_b = R.ln_e_b;
-    ea.eps = hp.eps;
-    ea.X = w.X;
-    ea.Xa = w.Xa;
-    LAUNCH_OK("embed_ln", launch_embed(wt, ea, (int)Mpad, st));
-
-    for (int il = 0; il < hp.n_layer; il++) {
+    if (!fused_qkv_attn && row0 != 0) {
+        set_err("internal: unfused attention with a row split");
+        return false;
+    }
+    {
         const DevLayer &L = R.L[il];
         GemmArgs q;
         q.A = w.Xa;
@@ -509,59 +489,149 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         if (fused_qkv_attn) {
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, n_seqs, st));
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, nseq, st));
         } else {
-            LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)Mpad, st));
-            LAUNCH_OK("attention", launch_attention(wt, D, aa, n_seqs, max_len, st));
+            LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
+            LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
         }
 
         GemmArgs o;
-        o.A = w.Ca;
+        o.A = Ca;
         o.K = E;
         o.W = L.o;
         o.N = E;
         o.bias = L.b_o;
-        o.X = w.X;
-        o.out_act = w.Xa;
+        o.X = X;
+        o.out_act = Xa;
         o.ln_w = L.ln1_w;
         o.ln_b = L.ln1_b;
         o.eps = hp.eps;
         if (ln_fused) {
-            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)Mpad, st));
+            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)rows, st));
         } else {
-            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)Mpad, st));
-            LAUNCH_OK("ln", launch_ln(wt, w.X, (int)Mpad, E, L.ln1_w, L.ln1_b, hp.eps, w.Xa, st));
+            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)rows, st));
+            LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
         }
 
         GemmArgs u;
-        u.A = w.Xa;
+        u.A = Xa;
         u.K = E;
         u.W = L.up;
         u.N = I;
         u.bias = L.b_up;
-        u.out_act = w.Ua;
+        u.out_act = Ua;
         u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
         u.gelu.n_pad = (int)tables().gelu_pair.size();  // the pair view (kernels.hip gelu_lookup)
         u.gelu.cap = tables().gelu_cap;
-        LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)Mpad, st));
+        LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)rows, st));
 
         GemmArgs dn;
-        dn.A = w.Ua;
+        dn.A = Ua;
         dn.K = I;
         dn.W = L.down;
         dn.N = E;
         dn.bias = L.b_down;
-        dn.X = w.X;
-        dn.out_act = w.Xa;
+        dn.X = X;
+        dn.out_act = Xa;
         dn.ln_w = L.ln2_w;
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
         if (ln_fused) {
-            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)Mpad, st));
+            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)rows, st));
         } else {
-            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)Mpad, st));
-            LAUNCH_OK("ln", launch_ln(wt, w.X, (int)Mpad, E, L.ln2_w, L.ln2_b, hp.eps, w.Xa, st));
+            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)rows, st));
+            LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
         }
+    }
+    return true;
+}
+
+// The fixed pipeline over a ragged batch already resident on the device.
+bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
+                  int n_seqs, float *d_out, hipStream_t st) {
+    const HParams &hp = ctx->hp;
+    const int64_t M = h_off[n_seqs];
+    const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
+    int max_len = 0;
+    for (int s = 0; s < n_seqs; s++) max_len = std::max(max_len, h_off[s + 1] - h_off[s]);
+    if (!ensure_workspace(ctx, R, Mpad, n_seqs)) return false;
+    Workspace &w = R.ws;
+    const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, wt = ctx->wtype;
+    const bool ln_fused = gemm_ln_fused(wt, E);
+    // QKV + attention in one kernel when every sentence fits one 128-row tile
+    // (env BERT_AMD_UNFUSED=1 forces the two-kernel path, for A/B checks)
+    static const bool force_unfused = std::getenv("BERT_AMD_UNFUSED") != nullptr;
+    const bool fused_qkv_attn = !force_unfused && qkv_attention_supported(wt, E, H, max_len);
+
+    EmbedArgs ea;
+    ea.tokens = d_tok;
+    ea.offsets = d_off;
+    ea.n_seqs = n_seqs;
+    ea.M = (int)M;
+    ea.E = E;
+    ea.n_vocab = hp.n_vocab;
+    ea.n_pos = hp.n_max_tokens;
+    ea.word = R.word;
+    ea.pos = R.pos;
+    ea.type = R.type;
+    ea.word_t = wtype_of(ctx->word_t);
+    ea.pos_t = wtype_of(ctx->pos_t);
+    ea.type_t = wtype_of(ctx->type_t);
+    ea.ln_w = R.ln_e_w;
+    ea.ln_b = R.ln_e_b;
+    ea.eps = hp.eps;
+    ea.X = w.X;
+    ea.Xa = w.Xa;
+    LAUNCH_OK("embed_ln", launch_embed(wt, ea, (int)Mpad, st));
+
+    // Row groups (opt-in, env BERT_AMD_SPLIT=1): with the fused QKV + attention
+    // path the batch is split at a 128-row-aligned sentence boundary near M / 2
+    // and the two halves run their layers on two streams, so one half's
+    // HBM-bound LayerNorm GEMMs can overlap the other half's MFMA / VALU-bound
+    // kernels.  Groups own disjoint rows of every buffer; sentences never span
+    // groups, so results are identical.  Measured +0.9 % on the north-star
+    // batch, within run-to-run noise, and it halves every
+    // launch, so it is off by default (per-kernel profiles stay full-batch).
+    struct Group {
+        int64_t row0, rows;  // rows: 128-multiple
+        int seq0, nseq;
+        hipStream_t s;
+    };
+    Group G[2] = {{0, Mpad, 0, n_seqs, st}, {0, 0, 0, 0, nullptr}};
+    int ng = 1;
+    static const bool split = std::getenv("BERT_AMD_SPLIT") != nullptr;
+    if (split && fused_qkv_attn && ln_fused && n_seqs >= 512 && R.stream2) {
+        int best = -1;
+        for (int s = 1; s < n_seqs; s++)
+            if (h_off[s] % GEMM_BM == 0 &&
+                (best < 0 || std::llabs(2LL * h_off[s] - M) < std::llabs(2LL * h_off[best] - M)))
+                best = s;
+        if (best > 0 && 4LL * h_off[best] >= M && 4LL * h_off[best] <= 3 * M) {
+            G[0] = {0, h_off[best], 0, best, st};
+            G[1] = {h_off[best], Mpad - h_off[best], best, n_seqs - best, R.stream2};
+            ng = 2;
+            HIP_OK(hipEventRecord(R.ev_fork, st));
+            HIP_OK(hipStreamWaitEvent(R.stream2, R.ev_fork, 0));
+        }
+    }
+    const size_t eb = act_elem_bytes(wt), sb = act_scale_bytes(wt);
+    auto act_rows = [&](ActPtr a, int64_t row0, int64_t K) {
+        a.q = (char *)a.q + row0 * K * (int64_t)eb;
+        if (a.d) a.d = (char *)a.d + row0 * (K / 32) * (int64_t)sb;
+        return a;
+    };
+
+    for (int il = 0; il < hp.n_layer; il++)
+        for (int gi = 0; gi < ng; gi++) {
+            const Group &gr = G[gi];
+            if (!run_layer(ctx, R, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, max_len, fused_qkv_attn,
+                           ln_fused, act_rows(w.Xa, gr.row0, E), act_rows(w.Ca, gr.row0, E),
+                           act_rows(w.Ua, gr.row0, I), w.X + gr.row0 * E, gr.s))
+                return false;
+        }
+    if (ng == 2) {
+        HIP_OK(hipEventRecord(R.ev_join, R.stream2));
+        HIP_OK(hipStreamWaitEvent(st, R.ev_join, 0));
     }
     LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st));
     return true;
@@ -609,6 +679,9 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
     R.device = device;
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&R.stream2, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
     auto &tr = R.weight_allocs;
     if (!upload(tr, &R.word, hm.word->data, hm.word->nbytes) || !upload(tr, &R.pos, hm.pos->data, hm.pos->nbytes) ||
         !upload(tr, &R.type, hm.type->data, hm.type->nbytes) ||
@@ -672,6 +745,12 @@ void free_replica(Replica &R) {
     if (R.ws.h_tok) hipHostFree(R.ws.h_tok);
     if (R.ws.h_off) hipHostFree(R.ws.h_off);
     if (R.ws.h_out) hipHostFree(R.ws.h_out);
+    if (R.stream2) {
+        hipStreamSynchronize(R.stream2);
+        hipStreamDestroy(R.stream2);
+    }
+    if (R.ev_fork) hipEventDestroy(R.ev_fork);
+    if (R.ev_join) hipEventDestroy(R.ev_join);
     if (R.stream) hipStreamDestroy(R.stream);
 }
 
