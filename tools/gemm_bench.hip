@@ -51,28 +51,6 @@ static void run(const char *name, GemmArgs a, int M, int iters) {
     fflush(stdout);
 }
 
-template <int WT, int EPI, int BN, int NW, int BM>
-static void run32(const char *name, GemmArgs a, int M, int iters) {
-    const int mt = M / BM, nt = a.N / BN;
-    auto launch = [&]() {
-        hipLaunchKernelGGL((gemm32_kernel<WT, EPI, BN, NW, BM>), dim3(mt * nt), dim3(NW * 64), 0, 0, a, mt, nt);
-    };
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0));
-    CK(hipEventCreate(&e1));
-    for (int i = 0; i < 3; i++) launch();
-    CK(hipGetLastError());
-    CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < iters; i++) launch();
-    CK(hipEventRecord(e1, 0));
-    CK(hipEventSynchronize(e1));
-    float ms;
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    const double us = ms * 1000.0 / iters, fl = 2.0 * M * (double)a.N * a.K;
-    printf("%-34s M=%d N=%d K=%d  %8.1f us  %6.1f TF/s (2MNK)\n", name, M, a.N, a.K, us, fl / us * 1e-6);
-    fflush(stdout);
-}
-
 int main(int argc, char **argv) {
     const int M = 131072, E = 384, I = 1536, iters = argc > 1 ? atoi(argv[1]) : 20;
     const int K_max = I, N_max = 3 * I;
@@ -172,16 +150,6 @@ int main(int argc, char **argv) {
                ms * 1000.0 / iters, z[0] / tot, z[1] / tot, z[2] / tot, z[3] / tot, tot / iters / S);
     }
 #endif
-    if (!strcmp(which, "g32")) {
-        run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   GELU <384,12,128>", u, M, iters);
-        run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
-        run32<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up32 GELU <384,12,128>", u, M, iters);
-        run32<W_Q4_0, EPI_NONE, 384, 12, 128>("up32 NONE <384,12,128>", u, M, iters);
-        run32<W_Q4_0, EPI_GELU_ACT, 256, 8, 128>("up32 GELU <256,8,128>", u, M, iters);
-        run32<W_Q4_0, EPI_NONE, 256, 8, 128>("up32 NONE <256,8,128>", u, M, iters);
-        run32<W_Q4_0, EPI_NONE, 384, 12, 128>("down32 NONE <384,12,128>", d, M, iters);
-        run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
-    }
     if (!strcmp(which, "gelu")) {
         run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   GELU <384,12,128>", u, M, iters);
         run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
