@@ -15,7 +15,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wn
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
 HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
 
-all: $(BUILD)/libbert.so
+all: $(BUILD)/libbert.so $(BUILD)/div_check
 
 $(BUILD)/obj/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/bert.h include/bert_amd.h
 	@mkdir -p $(dir $@)
@@ -41,3 +41,8 @@ clean:
 # development timing harness for the GEMM kernels (not shipped)
 $(BUILD)/gemm_bench: tools/gemm_bench.hip embedding.cpp_amd/csrc/kernels.hip embedding.cpp_amd/csrc/kernels.h
 	$(HIPCC) $(HIPFLAGS) $< -o $@
+
+# device check that the short Q8 scale divisions equal IEEE division (tests/test_gpu_parity.py)
+$(BUILD)/div_check: tools/div_check.hip
+	@mkdir -p $(BUILD)
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -Wno-unused-value -Wno-unused-result $< -o $@

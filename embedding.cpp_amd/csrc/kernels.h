@@ -67,6 +67,7 @@ enum Epi : int {
 // pattern (inf / NaN, non-identity positives) reads `full` in global memory.
 constexpr int HALF_TABLE_LDS = 36864;  // max compact GELU entries (72 KiB of LDS)
 constexpr int EXP_TABLE_LDS = 20480;   // max compact exp entries (40 KiB of LDS)
+constexpr int GELU_FLAT_LDS = 50480;  // Q4 FFN-up GEMM: GELU entries [0, 0x8000 + neg_n] (98.6 KiB of LDS)
 struct HalfTable {
     const uint16_t *full = nullptr;
     const uint16_t *compact = nullptr;  // n_pad entries, n_pad % 8 == 0
@@ -136,5 +137,9 @@ hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const
                      const ActPtr &out, hipStream_t s);
 bool gemm_shape_supported(int epi, int N, int K);
 bool gemm_ln_fused(int wtype, int N);  // false: EPI_RESID + launch_ln
+// true: the EPI_GELU_ACT weights are repacked in block-8 column order (repacked
+// tile 2p + t, fragment row r <- weight row 32p + 8(r >> 2) + 4t + (r & 3)), so
+// the transposed accumulators give each lane 8 adjacent columns of one row
+bool gemm_gelu_blk8(int wtype);
 
 }  // namespace bertamd

@@ -47,6 +47,30 @@ __device__ __forceinline__ uint32_t q8_pack4(float x0, float x1, float x2, float
     return lo | hi;
 }
 
+// Q8 block scales of ggml's quantize_row_q8_0/q8_1 (AVX2 form): d = amax / 127
+// and id = 127 / amax (0 when amax == 0), correctly rounded like the IEEE
+// divisions they replace: x / 127 by one Newton step on RN(1/127), and 127 / x
+// by one step on v_rcp_f32 inside [2^-101, 2^101) (outside it, the division).
+// tools/div_check.hip verifies both on the device for every positive finite
+// f32 (tests/test_gpu_parity.py::test_q8_scale_division_exhaustive).
+__device__ __forceinline__ float div127(float x) {
+    const float r = 1.0f / 127.0f;
+    const float q = x * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, 127.0f, x), r, q);
+}
+__device__ __forceinline__ float div127r(float x) {
+    const float y = __builtin_amdgcn_rcpf(x);
+    const float q = 127.0f * y;
+    return __builtin_fmaf(__builtin_fmaf(-x, q, 127.0f), y, q);
+}
+__device__ __forceinline__ void q8_scales(float amax, float &d, float &id) {
+    d = div127(amax);
+    if (__builtin_expect(amax >= 0x1p-101f && amax < 0x1p101f, 1))
+        id = div127r(amax);
+    else
+        id = amax != 0.f ? 127.f / amax : 0.f;
+}
+
 // ---------------------------------------------------------------------------
 // Activation block store: one 32-element block of one row, in the format the
 // next matmul consumes (ggml quantize_row_q8_0 / q8_1 AVX2 semantics:
@@ -57,8 +81,8 @@ __device__ __forceinline__ void store_act_block(const ActPtr &A, int64_t ld, int
         float amax = 0.f;
 #pragma unroll
         for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(v[j]));
-        const float d = amax / 127.f;
-        const float id = amax != 0.f ? 127.f / amax : 0.f;
+        float d, id;
+        q8_scales(amax, d, id);
         uint32_t pk[8];
 #pragma unroll
         for (int w = 0; w < 8; w++) pk[w] = q8_pack4(v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3], id);
@@ -98,8 +122,8 @@ __device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, i
         for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
         amax = fmaxf(amax, __shfl_xor(amax, 1));
         amax = fmaxf(amax, __shfl_xor(amax, 2));
-        const float d = amax / 127.f;
-        const float id = amax != 0.f ? 127.f / amax : 0.f;
+        float d, id;
+        q8_scales(amax, d, id);
         uint32_t pk[2];
 #pragma unroll
         for (int w = 0; w < 2; w++) pk[w] = q8_pack4(v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3], id);
@@ -119,6 +143,37 @@ __device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, i
         float4v *dst = (float4v *)((float *)A.q + row * ld + blk * 32 + 8 * qq);
         dst[0] = float4v{v[0], v[1], v[2], v[3]};
         dst[1] = float4v{v[4], v[5], v[6], v[7]};
+    }
+}
+
+// The same for a quarter held in the transposed MFMA layout: the four
+// quarters of a block are lanes c16, c16 + 16, c16 + 32, c16 + 48 (qq = lane
+// >> 4), so the amax is combined with the two row-swapping permutes (VALU, no
+// LDS round trip).
+template <int WT>
+__device__ __forceinline__ void store_act_quarter_t(const ActPtr &A, int64_t ld, int64_t row, int blk, int qq,
+                                                    const float *v) {
+    static_assert(WT == W_Q4_0 || WT == W_Q4_1, "Q8 activation formats only");
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
+    {
+        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+    }
+    {
+        const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+    }
+    float d, id;
+    q8_scales(amax, d, id);
+    const uint32_t p0 = q8_pack4(v[0], v[1], v[2], v[3], id), p1 = q8_pack4(v[4], v[5], v[6], v[7], id);
+    *(uint2 *)((int8_t *)A.q + row * ld + blk * 32 + 8 * qq) = make_uint2(p0, p1);
+    if (qq == 0) {
+        if constexpr (WT == W_Q4_0)
+            ((uint16_t *)A.d)[row * (ld / 32) + blk] = f2h(d);
+        else
+            ((float *)A.d)[row * (ld / 32) + blk] = d;
     }
 }
 
@@ -790,7 +845,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
-    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
+    // Q4 GELU: transposed accumulators in block-8 column order, epilogue in
+    // registers (gemm_gelu_blk8); otherwise 16-row LDS slices
+    constexpr bool GELU_T = QP && EPI == EPI_GELU_ACT;
+    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || GELU_T) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
     static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
@@ -799,20 +857,97 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
 #define GELU_LDS_TABLE 1
 #endif
     constexpr bool GT_LDS = GELU_LDS_TABLE && EPI == EPI_GELU_ACT;
-    __shared__ __attribute__((aligned(16))) uint16_t gtab[GT_LDS ? HALF_TABLE_LDS : 8];
+    __shared__ __attribute__((aligned(16))) uint16_t gtab[GT_LDS ? (GELU_T ? GELU_FLAT_LDS : HALF_TABLE_LDS) : 8];
 
     // XCD-aware tile order: linear block ids are dealt round-robin over the 8
     // XCDs; remap so that each XCD walks a contiguous range, n fastest, so the
     // N-tiles that share an A panel run on one XCD (bijective for any count).
-    const int nwg = n_mtiles * n_ntiles, orig = blockIdx.x;
-    const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int mt = lin / n_ntiles, ntile = lin - mt * n_ntiles;
+    // A persistent launch (GELU_T: gridDim.x a multiple of 8, each workgroup
+    // walking ids blockIdx.x + k * gridDim.x) keeps every id on its XCD.
+    const int nwg = n_mtiles * n_ntiles;
+    auto tile_of = [&](int orig, int64_t &m0_, int &n0_) {
+        const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+        const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+        const int mt = lin / n_ntiles;
+        m0_ = (int64_t)mt * BM;
+        n0_ = (lin - mt * n_ntiles) * BN;
+    };
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
-    const int64_t m0 = (int64_t)mt * BM;
-    const int n0 = ntile * BN;
+#ifndef GELU_T_EXP
+#define GELU_T_EXP 0
+#endif
+#ifndef GELU_T_PRE
+#define GELU_T_PRE 0
+#endif
+    if constexpr (GELU_T) {
+        // ggml's GELU table, entries [0, 0x8000 + neg_n] (every positive pattern,
+        // negatives up to the first of the constant run) -> LDS once per
+        // workgroup; inputs below -|h(neg_n)| are clamped onto that entry.
+        const int nflat8 = (0x8000 + args.gelu.neg_n + 1 + 7) / 8;
+        if (GELU_T_EXP != 3)
+            for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.full)[i];
+        const float xlo = h2f((uint16_t)(0x8000 | args.gelu.neg_n));
+        int64_t m0;
+        int n0;
+        tile_of(blockIdx.x, m0, n0);
+        MainloopPre<WT, NW, BM, NTW> pre;
+        mainloop_preload(pre, args, m0, (n0 + wv * WN) >> 4);
+        for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
+            float4v acc[RT][NTW];
+            gemm_mainloop<WT, NW, BM, NTW, true>(args, m0, (n0 + wv * WN) >> 4, smem, acc, pre);
+            const int64_t mc = m0;
+            const int nc = n0;
+#if GELU_T_PRE
+            if (t + (int)gridDim.x < nwg) {  // the next tile's first loads fly during this epilogue
+                tile_of(t + gridDim.x, m0, n0);
+                mainloop_preload(pre, args, m0, (n0 + wv * WN) >> 4);
+            }
+#endif
+            // Transposed accumulators over W repacked in block-8 order
+            // (gemm_gelu_blk8): lane (g, c16) holds acc[rt][2p + t][i] =
+            // C[mc + 16 rt + c16][32 pb + 8 g + 4 t + i] (pb = the pair's
+            // 32-column block), i.e. one quarter of one row's Q8 block.
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const int col = nc + wv * WN + 32 * p + 8 * g;
+                const float4v b0 = *(const float4v *)(args.bias + col), b1 = *(const float4v *)(args.bias + col + 4);
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++) {
+                    float y[8];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+#if GELU_T_EXP == 1  // timing experiment only: skip the table
+                        y[i] = b0[i] + acc[rt][2 * p][i];
+                        y[4 + i] = b1[i] + acc[rt][2 * p + 1][i];
+#else
+                        y[i] = h2f(gtab[f2h(fmaxf(b0[i] + acc[rt][2 * p][i], xlo))]);
+                        y[4 + i] = h2f(gtab[f2h(fmaxf(b1[i] + acc[rt][2 * p + 1][i], xlo))]);
+#endif
+                    }
+#if GELU_T_EXP == 2  // timing experiment only: no quantise / store
+                    float sum = 0.f;
+                    for (int i = 0; i < 8; i++) sum += y[i];
+                    if (sum == 1234.5678f) args.X[tid] = sum;
+#else
+                    store_act_quarter_t<WT>(args.out_act, args.N, mc + rt * 16 + c16, col >> 5, g, y);
+#endif
+                }
+            }
+#if !GELU_T_PRE
+            if (t + (int)gridDim.x < nwg) {
+                tile_of(t + gridDim.x, m0, n0);
+                mainloop_preload(pre, args, m0, (n0 + wv * WN) >> 4);
+            }
+#endif
+        }
+        return;
+    }
+
+    int64_t m0;
+    int n0;
+    tile_of(blockIdx.x, m0, n0);
     const int64_t ntile0 = (n0 + wv * WN) >> 4;
     if constexpr (GT_LDS) {  // GELU table -> LDS (read after the main loop's barriers)
         for (int i = tid; i < args.gelu.n_pad / 8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.compact)[i];
@@ -822,7 +957,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     {
         MainloopPre<WT, NW, BM, NTW> pre;
         mainloop_preload(pre, args, m0, ntile0);
-        gemm_mainloop<WT, NW, BM, NTW>(args, m0, ntile0, smem, acc, pre);
+#ifndef NONE_TRANS
+#define NONE_TRANS 0
+#endif
+        gemm_mainloop<WT, NW, BM, NTW, (NONE_TRANS && QP && EPI == EPI_NONE)>(args, m0, ntile0, smem, acc, pre);
     }
 
     // ---- epilogue, in registers.  Lane (g, c16), pair p, row-tile rt, i:
@@ -1058,8 +1196,8 @@ __device__ __forceinline__ void attn_store_ctx(const AttnArgs &a, float16v *o, f
 #pragma unroll
             for (int j = 0; j < 16; j++) amax = fmaxf(amax, fabsf(o[dt][j]));
             amax = fmaxf(amax, __shfl_xor(amax, 32));
-            const float d = amax / 127.f;
-            const float id = amax != 0.f ? 127.f / amax : 0.f;
+            float d, id;
+            q8_scales(amax, d, id);
             uint32_t pk[4];
 #pragma unroll
             for (int m = 0; m < 4; m++)
@@ -1637,10 +1775,26 @@ hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s) 
     return hipErrorInvalidValue;
 }
 
+static int n_cus() {
+    static int n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            c = 256;
+        return c;
+    }();
+    return n;
+}
+
 template <int WT, int EPI, int BN, int NW, int BM>
 static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
     const int mt = Mpad / BM, nt = a.N / BN;
-    hipLaunchKernelGGL((gemm_kernel<WT, EPI, BN, NW, BM>), dim3(mt * nt), dim3(NW * 64), 0, s, a, mt, nt);
+    int grid = mt * nt;
+    if constexpr ((WT == W_Q4_0 || WT == W_Q4_1) && EPI == EPI_GELU_ACT) {
+        // persistent: one workgroup per CU (the GELU table fills the LDS), a multiple of 8
+        if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS) return hipErrorInvalidValue;
+        grid = std::min(grid, std::max(8, n_cus() / 8 * 8));
+    }
+    hipLaunchKernelGGL((gemm_kernel<WT, EPI, BN, NW, BM>), dim3(grid), dim3(NW * 64), 0, s, a, mt, nt);
     return hipGetLastError();
 }
 
@@ -1682,6 +1836,8 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
 // Q4 weights: a 12-wave workgroup owns whole 384-wide rows; wider rows would
 // spill (two W blocks in flight x hi/lo), so they add the residual in the GEMM
 // and normalise in launch_ln.  F16 / F32 fuse LN up to 1024.
+bool gemm_gelu_blk8(int wtype) { return wtype == W_Q4_0 || wtype == W_Q4_1; }
+
 bool gemm_ln_fused(int wtype, int N) {
     if (wtype == W_Q4_0 || wtype == W_Q4_1) return N == 384;
     return N == 384 || N == 768 || N == 1024;

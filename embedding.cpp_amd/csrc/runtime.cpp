@@ -719,8 +719,18 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                     for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = rows[32 * pr + 16 * t + c];
             if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E))) return false;
         }
+        std::vector<const uint8_t *> up_rows = rows_of(l.i_w);
+        if (gemm_gelu_blk8(ctx->wtype)) {
+            // block-8 column order (kernels.h gemm_gelu_blk8): repack's interleave
+            // takes input row 32p + 2r + t to repacked row 16(2p + t) + r, which
+            // must hold weight row 32p + 8(r >> 2) + 4t + (r & 3)
+            const std::vector<const uint8_t *> src = up_rows;
+            for (size_t pr = 0; pr < src.size() / 32; pr++)
+                for (int t = 0; t < 2; t++)
+                    for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
+        }
         if (!upload_packed(tr, dl.qkv, repack(wt, rows, E)) || !upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E)) ||
-            !upload_packed(tr, dl.up, repack(wt, rows_of(l.i_w), E)) ||
+            !upload_packed(tr, dl.up, repack(wt, up_rows, E)) ||
             !upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I)))
             return false;
         if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||

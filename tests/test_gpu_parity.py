@@ -168,3 +168,15 @@ def test_encode_path_and_tokenizer(model_dir):
     assert ids[1][0] == 101 and ids[1][-1] == 102
     assert np.array_equal(emb, m.eval_batch(ids))
     assert np.array_equal(m.encode(texts[0]), emb[0])
+
+
+def test_q8_scale_division_exhaustive():
+    """kernels.hip q8_scales: the short forms of ggml's d = amax/127 and
+    id = 127/amax equal IEEE division for every positive finite f32 (the
+    reciprocal form inside [2^-101, 2^101), where the kernels use it)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "div_check")
+    assert os.path.exists(exe), "build/div_check missing: run make"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
+    print(out)
+    assert "x/127 mismatches 0;" in out and "127/x mismatches (x in [2^-101, 2^101)) 0," in out

@@ -33,7 +33,10 @@ template <int WT, int EPI, int BN, int NW, int BM>
 static void run(const char *name, GemmArgs a, int M, int iters) {
     const int mt = M / BM, nt = a.N / BN;
     auto launch = [&]() {
-        hipLaunchKernelGGL((gemm_kernel<WT, EPI, BN, NW, BM>), dim3(mt * nt), dim3(NW * 64), 0, 0, a, mt, nt);
+        if constexpr (EPI == EPI_NONE)
+            hipLaunchKernelGGL((gemm_kernel<WT, EPI, BN, NW, BM>), dim3(mt * nt), dim3(NW * 64), 0, 0, a, mt, nt);
+        else
+            CK((gemm_t<WT, EPI, BN, NW, BM>(a, M, 0)));  // the library's launch (persistent where it is)
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
