@@ -701,7 +701,10 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
 
     const float4v zero4 = {0.f, 0.f, 0.f, 0.f};
     for (int kc = 0; kc < nkc; kc++) {
-        const bool more = kc + 1 < nkc;
+#ifndef ML_EXP
+#define ML_EXP 0  // main-loop ablations (timing experiments only, wrong results): 2 no W reloads, 3 no A staging, 4 no barrier
+#endif
+        const bool more = kc + 1 < nkc && ML_EXP != 3;
         if (more) {
 #pragma unroll
             for (int it = 0; it < IT; it++) {
@@ -779,7 +782,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if (kc * KB + kb + 2 < nkb) {
+                if (kc * KB + kb + 2 < nkb && ML_EXP != 2) {
 #pragma unroll
                     for (int nt = 0; nt < NTW; nt++)
                         wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
@@ -827,7 +830,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 if (item < ITEMS) a_store<WT, BM>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
-        __syncthreads();
+        if (ML_EXP != 4) __syncthreads();
     }
 
 }

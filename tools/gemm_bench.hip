@@ -153,6 +153,7 @@ int main(int argc, char **argv) {
                ms * 1000.0 / iters, z[0] / tot, z[1] / tot, z[2] / tot, z[3] / tot, tot / iters / S);
     }
 #endif
+    if (!strcmp(which, "upnone")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
     if (!strcmp(which, "gelu")) {
         run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   GELU <384,12,128>", u, M, iters);
         run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
