@@ -101,6 +101,7 @@ struct GemmArgs {
 struct EmbedArgs {
     const int32_t *tokens = nullptr;   // [M] packed
     const int32_t *offsets = nullptr;  // [n_seqs+1]
+    int32_t *rowpos = nullptr;         // [M] scratch: position of each packed row in its sentence
     int n_seqs = 0, M = 0, E = 0, n_vocab = 0, n_pos = 0;
     const void *word = nullptr, *pos = nullptr, *type = nullptr;  // ggml row format of `ttype`
     int word_t = 0, pos_t = 0, type_t = 0;

@@ -346,6 +346,14 @@ __device__ __forceinline__ void table8(const void *tab, int type, int64_t row, i
 // 16 rows per workgroup, four lanes per (row, 32-element block) like the GEMM
 // LayerNorm epilogue (ln_row_phase_q): values stay in registers, statistics
 // in double combined quarter -> block (shuffles) -> row (fixed block order).
+// Position of every packed row inside its sentence (positions 0..n-1,
+// bert.cpp:874-878), one workgroup per sentence: embed_ln_kernel then reads
+// it instead of searching the offsets per row.
+__global__ __launch_bounds__(128) void row_pos_kernel(const int32_t *__restrict__ offsets, int32_t *__restrict__ rowpos) {
+    const int s = blockIdx.x, beg = offsets[s], end = offsets[s + 1];
+    for (int r = beg + (int)threadIdx.x; r < end; r += 128) rowpos[r] = r - beg;
+}
+
 template <int WT, int NBLK>
 __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
     constexpr int E = NBLK * 32, TPT = 64 * NBLK / 256;  // tasks per thread
@@ -357,13 +365,8 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
         const int64_t row = row0 + tid;
         int tok = -1, pos = 0;
         if (row < a.M) {
-            int lo = 0, hi = a.n_seqs;  // largest s with offsets[s] <= row
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (a.offsets[mid] <= row) lo = mid; else hi = mid;
-            }
             tok = min(max(a.tokens[row], 0), a.n_vocab - 1);  // ids are validated on the host path;
-            pos = min((int)(row - a.offsets[lo]), a.n_pos - 1); // clamp keeps device-fed ids in bounds
+            pos = min(a.rowpos[row], a.n_pos - 1);              // clamp keeps device-fed ids in bounds
         }
         rinfo[2 * tid] = tok;
         rinfo[2 * tid + 1] = pos;
@@ -1759,6 +1762,7 @@ __global__ __launch_bounds__(256) void pool_l2_kernel(const float *X, const int3
 // launchers
 template <int WT>
 static hipError_t embed_t(const EmbedArgs &a, int Mpad, hipStream_t s) {
+    if (a.n_seqs > 0) hipLaunchKernelGGL(row_pos_kernel, dim3(a.n_seqs), dim3(128), 0, s, a.offsets, a.rowpos);
     switch (a.E) {
         case 384: hipLaunchKernelGGL((embed_ln_kernel<WT, 12>), dim3(Mpad / 16), dim3(256), 0, s, a); break;
         case 768: hipLaunchKernelGGL((embed_ln_kernel<WT, 24>), dim3(Mpad / 16), dim3(256), 0, s, a); break;

@@ -178,7 +178,7 @@ struct Workspace {
     float *X = nullptr, *out = nullptr;
     uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16: kernels.h GemmArgs EPI_QKV
     ActPtr Xa, Ca, Ua;
-    int32_t *tok = nullptr, *off = nullptr;
+    int32_t *tok = nullptr, *off = nullptr, *rowpos = nullptr;
     std::vector<void *> allocs;
     // pinned host staging for the host-pointer ABI
     int32_t *h_tok = nullptr, *h_off = nullptr;
@@ -386,7 +386,8 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs) {
         !dmalloc(w.allocs, &w.vt_lo, (size_t)rows * E * 2) ||
         !alloc_act(w.allocs, w.Xa, wt, rows, E) || !alloc_act(w.allocs, w.Ca, wt, rows, E) ||
         !alloc_act(w.allocs, w.Ua, wt, rows, I) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
-        !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4))
+        !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4) ||
+        !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4))
         return false;
     // padding rows must hold finite values: zero everything once
     HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, R.stream));
@@ -566,6 +567,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     EmbedArgs ea;
     ea.tokens = d_tok;
     ea.offsets = d_off;
+    ea.rowpos = w.rowpos;
     ea.n_seqs = n_seqs;
     ea.M = (int)M;
     ea.E = E;
