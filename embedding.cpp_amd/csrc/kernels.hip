@@ -219,6 +219,13 @@ __device__ __forceinline__ void ln_tasks(LnTask (&tk)[64 * NBLK / NT], int tid, 
 template <int NBLK, int NT>
 __device__ __forceinline__ void ln_xload(float4v (&xv)[64 * NBLK / NT][2], const LnTask (&tk)[64 * NBLK / NT],
                                          const float *X, int64_t row0) {
+#ifndef LN_EXP
+#define LN_EXP 0  // LN epilogue ablations (timing experiments only, wrong results): 1 no residual loads, 2 no stores, 3 no Q8 stores
+#endif
+#if LN_EXP == 1
+    for (int k = 0; k < 64 * NBLK / NT; k++) xv[k][0] = xv[k][1] = float4v{0.f, 0.f, 0.f, 0.f};
+    return;
+#endif
 #pragma unroll
     for (int k = 0; k < 64 * NBLK / NT; k++) {
         const float4v *xp = (const float4v *)(X + (row0 + tk[k].r) * (int64_t)(NBLK * 32) + tk[k].c);
@@ -298,10 +305,18 @@ __device__ __forceinline__ void ln_row_phase_q(float *stage, int ld, double *red
                 y[4 * h + j] = z + lb[j];
             }
         }
+#if LN_EXP == 2  // timing experiment only: no stores
+        float sum = 0.f;
+        for (int i = 0; i < 8; i++) sum += y[i];
+        if (sum == 1234.5678f) X[threadIdx.x] = sum;
+#else
         float4v *xo = (float4v *)(X + (row0 + tk[k].r) * (int64_t)ncols + tk[k].c);
         xo[0] = float4v{y[0], y[1], y[2], y[3]};
         xo[1] = float4v{y[4], y[5], y[6], y[7]};
+#if LN_EXP != 3  // 3: X stores only
         store_act_quarter<WT>(out, ncols, row0 + tk[k].r, tk[k].b, tk[k].qq, y);
+#endif
+#endif
     }
 }
 
