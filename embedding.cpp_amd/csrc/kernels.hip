@@ -242,19 +242,20 @@ __device__ __forceinline__ void ln_row_phase_q(float *stage, int ld, double *red
                                                float eps, const ActPtr &out) {
     constexpr int ncols = NBLK * 32, TPT = 64 * NBLK / NT;
     double *red1 = red, *red2 = red + 16 * NBLK;
+    float4v vv[TPT][2];  // the task's values between the passes (registers, not the stage)
 #pragma unroll
     for (int k = 0; k < TPT; k++) {
-        float *sp = stage + tk[k].r * ld + tk[k].c;
+        const float *sp = stage + tk[k].r * ld + tk[k].c;
         double s = 0.0;
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            float4v v = *(float4v *)(sp + 4 * h);
+            float4v v = *(const float4v *)(sp + 4 * h);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 v[j] = (tk[k].bias[h][j] + v[j]) + xv[k][h][j];
                 s += (double)v[j];
             }
-            *(float4v *)(sp + 4 * h) = v;
+            vv[k][h] = v;
         }
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
@@ -267,17 +268,15 @@ __device__ __forceinline__ void ln_row_phase_q(float *stage, int ld, double *red
 #pragma unroll
         for (int q = 0; q < NBLK; q++) tot += red1[tk[k].r * NBLK + q];
         const float mean = (float)(tot / ncols);
-        float *sp = stage + tk[k].r * ld + tk[k].c;
         double s2 = 0.0;
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            float4v v = *(float4v *)(sp + 4 * h);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                v[j] = v[j] - mean;
-                s2 += (double)(v[j] * v[j]);
+                const float v = vv[k][h][j] - mean;
+                vv[k][h][j] = v;
+                s2 += (double)(v * v);
             }
-            *(float4v *)(sp + 4 * h) = v;
         }
         s2 += __shfl_xor(s2, 1);
         s2 += __shfl_xor(s2, 2);
@@ -291,11 +290,10 @@ __device__ __forceinline__ void ln_row_phase_q(float *stage, int ld, double *red
         for (int q = 0; q < NBLK; q++) tot += red2[tk[k].r * NBLK + q];
         const float var = (float)(tot / ncols);
         const float scale = 1.0f / sqrtf(var + eps);
-        const float *sp = stage + tk[k].r * ld + tk[k].c;
         float y[8];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            const float4v v = *(const float4v *)(sp + 4 * h);
+            const float4v v = vv[k][h];
             const float4v w = *(const float4v *)(lnw + tk[k].c + 4 * h);
             const float4v lb = *(const float4v *)(lnb + tk[k].c + 4 * h);
 #pragma unroll
@@ -869,7 +867,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     // Q4 GELU: transposed accumulators in block-8 column order, epilogue in
     // registers (gemm_gelu_blk8); otherwise 16-row LDS slices
     constexpr bool GELU_T = QP && EPI == EPI_GELU_ACT;
-    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || GELU_T) ? 0 : 16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0);
+    // LN: two 16-row slice buffers (stage + row partials) for BN <= 768
+    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || GELU_T) ? 0 : (EPI == EPI_LN && BN <= 768 ? 2 : 1) * (16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0));
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
     static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
@@ -1058,8 +1057,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         // is odd in 16-byte slots, so the 16 lanes reading one block of 16 rows
         // hit 16 slots.
         constexpr int LD = BN + 4, NBLK = BN / 32, TPT = 64 * NBLK / NT;
-        float *stage = (float *)smem;
-        double *red = (double *)(smem + 16 * LD * 4);  // [2][16][NBLK]
+        constexpr int SLICE_BYTES = 16 * LD * 4 + ((EPI == EPI_LN) ? 2 * 16 * NBLK * 8 : 0);
+        constexpr int NSB = (EPI == EPI_LN && 2 * SLICE_BYTES <= SMEM) ? 2 : 1;  // LN: stage + red double-buffered
         constexpr bool LN = EPI == EPI_LN;
         [[maybe_unused]] LnTask tk[LN ? TPT : 1];
         [[maybe_unused]] float4v xv[2][LN ? TPT : 1][2];
@@ -1077,7 +1076,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         }
 #pragma unroll
         for (int rt = 0; rt < RT; rt++) {
-            __syncthreads();
+            // with two slice buffers the previous slice's readers never share a buffer with this
+            // slice's writers, except across one full slice (whose own barriers separate them)
+            float *stage = (float *)(smem + (rt % NSB) * SLICE_BYTES);
+            double *red = (double *)(smem + (rt % NSB) * SLICE_BYTES + 16 * LD * 4);  // [2][16][NBLK]
+            if (NSB == 1 || rt == 0) __syncthreads();
 #pragma unroll
             for (int p = 0; p < NP; p++)
 #pragma unroll
