@@ -1546,7 +1546,10 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
                 }
                 mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
-                double sum = 0.0;
+                // ggml's double sum of the fp16 probabilities, exactly: every p is a
+                // multiple of 2^-24 in [0, 1], so p * 2^24 is an integer and the
+                // sum of n <= 128 of them fits a uint32
+                uint32_t sum = 0;
                 float16v o[D / 32];
 #pragma unroll
                 for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
@@ -1555,16 +1558,18 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     half8 ph[2];
 #pragma unroll
                     for (int j = 0; j < 16; j++) {
-                        // ggml_scale after K.Q, then p = exp_tab[fp16(s - max)] (s - max <= 0; -inf -> 0)
-                        const uint32_t hm = f2h(S[j] * a.scale - mx) & 0x7fffu;
+                        // ggml_scale after K.Q, then p = exp_tab[fp16(s - max)]: s - max <= 0, and
+                        // fp16(max - s) is its magnitude exactly (IEEE subtraction is sign-symmetric;
+                        // masked keys: +inf -> the constant-0 entry)
+                        const uint32_t hm = f2h(mx - S[j] * a.scale);
                         const uint16_t pb = etab[epos + min(hm, (uint32_t)eneg)];
                         ph[j >> 3][j & 7] = __builtin_bit_cast(_Float16, pb);
-                        sum += (double)h2f(pb);
+                        sum += (uint32_t)(h2f(pb) * 16777216.0f);
                     }
                     attn_pv_h<D>(o, Vh, Vl, VST, 32 * kt, r, hh, ph);
                 }
                 sum += __shfl_xor(sum, 32);
-                attn_store_ctx<WT, D>(a, o, (float)(1.0 / sum), beg + q0 + r, q0 + r < n, head, hh);
+                attn_store_ctx<WT, D>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + q0 + r, q0 + r < n, head, hh);
             }
         }
         __syncthreads();  // the next pair's A chunks overwrite the attention tiles
