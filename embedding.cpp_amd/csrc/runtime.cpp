@@ -576,9 +576,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     ea.word = R.word;
     ea.pos = R.pos;
     ea.type = R.type;
-    ea.word_t = wtype_of(ctx->word_t);
-    ea.pos_t = wtype_of(ctx->pos_t);
-    ea.type_t = wtype_of(ctx->type_t);
+    ea.word_t = ea.pos_t = ea.type_t = W_F32;  // the replica holds f32 copies (table_f32)
     ea.ln_w = R.ln_e_w;
     ea.ln_b = R.ln_e_b;
     ea.eps = hp.eps;
@@ -677,6 +675,42 @@ struct HostModel {
     std::vector<L> layers;
 };
 
+// An embedding table as f32 rows, exactly as ggml_get_rows dequantises it
+// (reference bert.cpp:880-887): F16 widened, Q4_0
+// (q - 8) * d, Q4_1 q * d + m (one fused multiply-add, as ggml's compiled
+// dequantize_row_q4_1).  The device keeps the f32 copy, so the gather is a
+// plain row read (the quantised rows would cost five narrow loads per 8 values).
+std::vector<float> table_f32(const GGUFTensor *t) {
+    const int64_t E = t->ne[0], rows = t->nrows();
+    std::vector<float> out((size_t)(E * rows));
+    for (int64_t r = 0; r < rows; r++) {
+        float *o = &out[(size_t)(r * E)];
+        if (t->type == GT_F32) {
+            std::memcpy(o, t->data + r * E * 4, (size_t)E * 4);
+        } else if (t->type == GT_F16) {
+            const uint16_t *h = (const uint16_t *)(t->data + r * E * 2);
+            for (int64_t e = 0; e < E; e++) o[e] = f16_to_f32(h[e]);
+        } else {
+            const bool q1 = t->type == GT_Q4_1;
+            const int bs = q1 ? 20 : 18;
+            const uint8_t *row = t->data + r * (E / 32) * bs;
+            for (int64_t b = 0; b < E / 32; b++) {
+                const uint8_t *blk = row + b * bs;
+                uint16_t dh, mh = 0;
+                std::memcpy(&dh, blk, 2);
+                if (q1) std::memcpy(&mh, blk + 2, 2);
+                const float d = f16_to_f32(dh), m = f16_to_f32(mh);
+                const uint8_t *qs = blk + (q1 ? 4 : 2);
+                for (int j = 0; j < 32; j++) {
+                    const int q = j < 16 ? (qs[j] & 15) : (qs[j - 16] >> 4);
+                    o[b * 32 + j] = q1 ? std::fmaf((float)q, d, m) : (float)(q - 8) * d;
+                }
+            }
+        }
+    }
+    return out;
+}
+
 bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
     R.device = device;
     HIP_OK(hipSetDevice(device));
@@ -685,8 +719,9 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
     HIP_OK(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
     auto &tr = R.weight_allocs;
-    if (!upload(tr, &R.word, hm.word->data, hm.word->nbytes) || !upload(tr, &R.pos, hm.pos->data, hm.pos->nbytes) ||
-        !upload(tr, &R.type, hm.type->data, hm.type->nbytes) ||
+    const std::vector<float> word = table_f32(hm.word), pos = table_f32(hm.pos), type = table_f32(hm.type);
+    if (!upload(tr, &R.word, word.data(), word.size() * 4) || !upload(tr, &R.pos, pos.data(), pos.size() * 4) ||
+        !upload(tr, &R.type, type.data(), type.size() * 4) ||
         !upload(tr, &R.ln_e_w, hm.ln_e_w->data, hm.ln_e_w->nbytes) ||
         !upload(tr, &R.ln_e_b, hm.ln_e_b->data, hm.ln_e_b->nbytes) ||
         !upload(tr, &R.gelu_tab, tables().gelu.data(), 65536 * 2) ||
