@@ -1370,22 +1370,25 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
             }
         }
         mx = fmaxf(mx, __shfl_xor(mx, 32));
-        double sum = 0.0;
+        // ggml's double sum of the fp16 probabilities, exactly: p * 2^24 is an
+        // integer for every fp16 p in [0, 1], and n <= 128 of them fit a uint32
+        uint32_t sum = 0;
 #pragma unroll
         for (int kt = 0; kt < 4; kt++) {
             if (kt < nkt) {
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
-                    // s - max <= 0: exp_tab[fp16(s - max)] from LDS; -inf (masked) -> 0
-                    const uint32_t hm = f2h(S[kt][j] - mx) & 0x7fffu;
+                    // s - max <= 0: exp_tab[fp16(s - max)] from LDS, indexed by the
+                    // magnitude fp16(max - s); -inf (masked) -> +inf -> the 0 entry
+                    const uint32_t hm = f2h(mx - S[kt][j]);
                     const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
                     S[kt][j] = p;
-                    sum += (double)p;
+                    sum += (uint32_t)(p * 16777216.0f);
                 }
             }
         }
         sum += __shfl_xor(sum, 32);
-        const float rs = (float)(1.0 / sum);
+        const float rs = (float)(1.0 / ((double)sum * 0x1p-24));
         float16v o[D / 32];
 #pragma unroll
         for (int dt = 0; dt < D / 32; dt++) o[dt] = zero16;
@@ -1699,7 +1702,7 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
     };
     const int nch = (n + NK - 1) / NK;
     float mx = -INFINITY;
-    double sum = 0.0;
+    uint64_t sum = 0;  // the probabilities' exact sum in units of 2^-24 (as in attention_short_kernel)
     float16v o[D / 32];
 #pragma unroll
     for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
@@ -1722,19 +1725,22 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
 #pragma unroll
                 for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
             } else {    // pass 2: p, sum, P.V
+                uint32_t part = 0;  // 16 terms <= 2^24
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
-                    const uint32_t hm = f2h(S[j] - mx) & 0x7fffu;  // s - max <= 0; -inf -> 0
+                    const uint32_t hm = f2h(mx - S[j]);  // |s - max| as fp16; masked -inf -> +inf -> 0
                     const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
                     S[j] = p;
-                    sum += (double)p;
+                    part += (uint32_t)(p * 16777216.0f);
                 }
+                sum += part;
                 attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
             }
         }
     }
-    sum += __shfl_xor(sum, 32);
-    if (active) attn_store_ctx<WT, D>(a, o, (float)(1.0 / sum), beg + q0 + r, q0 + r < n, h, hh);
+    double tot = (double)sum * 0x1p-24;  // exact (< 2^34 units), and so is the pair sum
+    tot += __shfl_xor(tot, 32);
+    if (active) attn_store_ctx<WT, D>(a, o, (float)(1.0 / tot), beg + q0 + r, q0 + r < n, h, hh);
 }
 
 // ---------------------------------------------------------------------------
