@@ -18,11 +18,11 @@ step() {  # name seconds cmd...
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
 B="$PWD/bench.py"
-step bench 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 64
+step bench 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 256
 step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o $TAG -- python3 "$B" --steps 10 --warmup 3 --cpu-sample 0
 step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0
 step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0
 F=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -1)
 W=$(find "$OUT/write" -name '*counter_collection.csv' | head -1)
-step bench_pmc 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 64 --pmc-csv "$F,$W"
+step bench_pmc 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 256 --pmc-csv "$F,$W"
 tail -1 "$OUT/bench_pmc.log"
