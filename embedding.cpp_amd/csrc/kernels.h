@@ -132,6 +132,8 @@ hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs
 // QKV GEMM + attention in one kernel (sentences <= 128 tokens, head dim 32);
 // g: the QKV GemmArgs (head-major weights), a: the AttnArgs (its Q/K/V pointers unused)
 bool qkv_attention_supported(int wtype, int E, int H, int max_len);
+// head pairs per GEMM main loop of that kernel (its QKV copy's tile grouping, runtime.cpp)
+int qkv_attention_ntw(int wtype);
 hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s);
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s);
 hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const float *b, float eps,

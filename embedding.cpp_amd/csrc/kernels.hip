@@ -1403,7 +1403,8 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 // n <= 128 tokens and heads of D = 32 (MiniLM): one 12-wave workgroup per
 // sentence, so Q, K and V (hi/lo, 4 bytes a value) never leave the CU —
 // the unfused pair writes and re-reads 12 bytes per token and feature.
-// Heads go two at a time: the GEMM main loop (gemm_mainloop, the 128 rows
+// Heads go four at a time (Q4; two for F16) through the GEMM main loop (one
+// n-tile per wave and head pair) and two at a time through the attention tiles: the main loop (gemm_mainloop, the 128 rows
 // from the sentence's first token) computes the pair's 192 head-major QKV
 // features (kernels.h GemmArgs), one 16-feature n-tile per wave; b + W.x is
 // split hi/lo into the two heads' attention tiles in LDS, and the 8
@@ -1425,9 +1426,10 @@ __device__ unsigned long long qkva_prof[4];
 
 template <int WT>
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
-    constexpr int D = QKVA_D, NW = QKVA_NW, BM = 128, NTW = 1, RT = BM / 16;
-    constexpr int NK = 128, KST = D + 8, VST = NK + 4;
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr int D = QKVA_D, NW = QKVA_NW, BM = 128, RT = BM / 16;
+    constexpr int NTW = QP ? 2 : 1;  // head pairs per main loop (qkv_attention_ntw)
+    constexpr int NK = 128, KST = D + 8, VST = NK + 4;
     constexpr int A_BUF = (WT == W_F32 ? BM * LDA_F * 4 : BM * LDA_H * 2) + (QP ? KB * BM * 4 : 0);
     constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
     constexpr int SMEM = (2 * A_BUF > 2 * SLOT) ? 2 * A_BUF : 2 * SLOT;
@@ -1459,123 +1461,133 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     uint64_t t_last = __builtin_amdgcn_s_memtime();
 #endif
 
-    for (int pr = 0; pr < a.H / 2; pr++) {
-        const int fpair = pr * 6 * D;  // first head-major feature of the pair
+    for (int qd = 0; qd < a.H / (2 * NTW); qd++) {
+        // heads 2 NTW qd ..: one main loop (one pass over the sentence's A panel)
+        // serves NTW head pairs.  g.W is in grouped tile order (runtime.cpp): wave
+        // w's n-tiles nt0 + t are n-tile w of pair NTW qd + t, so acc[..][half]
+        // plays the one-pair role of the split below.  (NTW = 2 for F16 measured
+        // 28 % faster but fails parity, DESIGN.md §3: F16 stays at one pair.)
+        const int64_t nt0 = (int64_t)qd * NTW * NW + NTW * wv;
         float4v acc[RT][NTW];
         QKVA_MARK(0);
-        MainloopPre<WT, NW, BM, NTW> pre;  // (loading it during the previous pair's attention measured no faster)
-        mainloop_preload(pre, g, beg, (fpair >> 4) + wv);
+        MainloopPre<WT, NW, BM, NTW> pre;
+        mainloop_preload(pre, g, beg, nt0);
         if (part_w == 2)  // ends with a barrier
-            gemm_mainloop<WT, NW, BM, NTW, false>(g, beg, (fpair >> 4) + wv, smem, acc, pre);
+            gemm_mainloop<WT, NW, BM, NTW, false>(g, beg, nt0, smem, acc, pre);
         else
-            gemm_mainloop<WT, NW, BM, NTW, true>(g, beg, (fpair >> 4) + wv, smem, acc, pre);
+            gemm_mainloop<WT, NW, BM, NTW, true>(g, beg, nt0, smem, acc, pre);
         QKVA_MARK(1);
-        {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values).
-            // LDS byte offsets and row limits are rebuilt per pair behind opaque
-            // moves, so the compiler does not hoist addresses / row masks out of
-            // the pair loop (register pressure: they were spilled to scratch).
-            if (part_w == 2) {
-                const float b = g.bias[fpair + 16 * wv + c16];
-                int rl = n - 4 * gq;  // row 16 rt + 4 gq + i is valid while 16 rt + i < rl
-                asm volatile("" : "+v"(rl));
-                uint32_t off = (uint32_t)((char *)slot(hs_w, 4) - smem) + (uint32_t)((d0 + c16) * VST + 4 * gq) * 2;
-                asm volatile("" : "+v"(off));
 #pragma unroll
-                for (int rt = 0; rt < RT; rt++) {
-                    half4v hv, lv;
+        for (int half = 0; half < NTW; half++) {
+            const int pr = NTW * qd + half;
+            const int fpair = pr * 6 * D;  // first head-major feature of the pair
+            {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values).
+                // LDS byte offsets and row limits are rebuilt per pair behind opaque
+                // moves, so the compiler does not hoist addresses / row masks out of
+                // the pair loop (register pressure: they were spilled to scratch).
+                if (part_w == 2) {
+                    const float b = g.bias[fpair + 16 * wv + c16];
+                    int rl = n - 4 * gq;  // row 16 rt + 4 gq + i is valid while 16 rt + i < rl
+                    asm volatile("" : "+v"(rl));
+                    uint32_t off = (uint32_t)((char *)slot(hs_w, 4) - smem) + (uint32_t)((d0 + c16) * VST + 4 * gq) * 2;
+                    asm volatile("" : "+v"(off));
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const float y = rt * 16 + i < rl ? b + acc[rt][0][i] : 0.f;
-                        hv[i] = (_Float16)y;
-                        lv[i] = (_Float16)(y - (float)hv[i]);
+                    for (int rt = 0; rt < RT; rt++) {
+                        half4v hv, lv;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const float y = rt * 16 + i < rl ? b + acc[rt][half][i] : 0.f;
+                            hv[i] = (_Float16)y;
+                            lv[i] = (_Float16)(y - (float)hv[i]);
+                        }
+                        *(half4v *)(smem + off + rt * 32) = hv;
+                        *(half4v *)(smem + off + D * VST * 2 + rt * 32) = lv;
                     }
-                    *(half4v *)(smem + off + rt * 32) = hv;
-                    *(half4v *)(smem + off + D * VST * 2 + rt * 32) = lv;
-                }
-            } else {
-                const float4v b4 = *(const float4v *)(g.bias + fpair + 16 * wv + 4 * gq);
-                int rl = n - c16;  // row 16 rt + c16 is valid while 16 rt < rl
-                asm volatile("" : "+v"(rl));
-                uint32_t off = (uint32_t)((char *)slot(hs_w, 2 * part_w) - smem) + (uint32_t)(c16 * KST + d0 + 4 * gq) * 2;
-                asm volatile("" : "+v"(off));
+                } else {
+                    const float4v b4 = *(const float4v *)(g.bias + fpair + 16 * wv + 4 * gq);
+                    int rl = n - c16;  // row 16 rt + c16 is valid while 16 rt < rl
+                    asm volatile("" : "+v"(rl));
+                    uint32_t off = (uint32_t)((char *)slot(hs_w, 2 * part_w) - smem) + (uint32_t)(c16 * KST + d0 + 4 * gq) * 2;
+                    asm volatile("" : "+v"(off));
 #pragma unroll
-                for (int rt = 0; rt < RT; rt++) {
-                    half4v hv, lv;
+                    for (int rt = 0; rt < RT; rt++) {
+                        half4v hv, lv;
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const float y = rt * 16 < rl ? b4[i] + acc[rt][0][i] : 0.f;
-                        hv[i] = (_Float16)y;
-                        lv[i] = (_Float16)(y - (float)hv[i]);
+                        for (int i = 0; i < 4; i++) {
+                            const float y = rt * 16 < rl ? b4[i] + acc[rt][half][i] : 0.f;
+                            hv[i] = (_Float16)y;
+                            lv[i] = (_Float16)(y - (float)hv[i]);
+                        }
+                        *(half4v *)(smem + off + rt * 16 * KST * 2) = hv;
+                        *(half4v *)(smem + off + NK * KST * 2 + rt * 16 * KST * 2) = lv;
                     }
-                    *(half4v *)(smem + off + rt * 16 * KST * 2) = hv;
-                    *(half4v *)(smem + off + NK * KST * 2 + rt * 16 * KST * 2) = lv;
                 }
             }
-        }
-        __syncthreads();
-        QKVA_MARK(2);
+            __syncthreads();
+            QKVA_MARK(2);
 
-        if (wv < 8) {  // attention task (head slot, 32 queries)
-            const int hs = wv >> 2, q0 = (wv & 3) * 32, head = 2 * pr + hs;
-            if (q0 < n) {
-                const _Float16 *Qh = slot(hs, 0), *Ql = slot(hs, 1), *Kh = slot(hs, 2), *Kl = slot(hs, 3);
-                const _Float16 *Vh = slot(hs, 4), *Vl = slot(hs, 5);
-                half8 qh[D / 16], ql[D / 16];
+            if (wv < 8) {  // attention task (head slot, 32 queries)
+                const int hs = wv >> 2, q0 = (wv & 3) * 32, head = 2 * pr + hs;
+                if (q0 < n) {
+                    const _Float16 *Qh = slot(hs, 0), *Ql = slot(hs, 1), *Kh = slot(hs, 2), *Kl = slot(hs, 3);
+                    const _Float16 *Vh = slot(hs, 4), *Vl = slot(hs, 5);
+                    half8 qh[D / 16], ql[D / 16];
 #pragma unroll
-                for (int ks = 0; ks < D / 16; ks++) {
-                    qh[ks] = *(const half8 *)(Qh + (q0 + r) * KST + 16 * ks + 8 * hh);
-                    ql[ks] = *(const half8 *)(Ql + (q0 + r) * KST + 16 * ks + 8 * hh);
-                }
-                // two passes over the key tiles (the second recomputes the identical
-                // scores): only one 32-key score tile is live, which keeps this
-                // phase inside the 12-wave register budget next to the GEMM's.
-                // Pass 1 takes the max of the unscaled K.Q: x -> fl(x * scale) is
-                // monotonic for scale > 0, so fl(max * scale) is ggml's max of the
-                // scaled scores.
-                const int nkt = (n + 31) >> 5;
-                auto scores = [&](int kt) {
-                    float16v S = attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql);
-                    if (32 * kt + 32 > n) {
-#pragma unroll
-                        for (int j = 0; j < 16; j++)
-                            if (32 * kt + (j & 3) + 8 * (j >> 2) >= lim) S[j] = -INFINITY;
+                    for (int ks = 0; ks < D / 16; ks++) {
+                        qh[ks] = *(const half8 *)(Qh + (q0 + r) * KST + 16 * ks + 8 * hh);
+                        ql[ks] = *(const half8 *)(Ql + (q0 + r) * KST + 16 * ks + 8 * hh);
                     }
-                    return S;
-                };
-                float mx = -INFINITY;
-                for (int kt = 0; kt < nkt; kt++) {
-                    const float16v S = scores(kt);
+                    // two passes over the key tiles (the second recomputes the identical
+                    // scores): only one 32-key score tile is live, which keeps this
+                    // phase inside the 12-wave register budget next to the GEMM's.
+                    // Pass 1 takes the max of the unscaled K.Q: x -> fl(x * scale) is
+                    // monotonic for scale > 0, so fl(max * scale) is ggml's max of the
+                    // scaled scores.
+                    const int nkt = (n + 31) >> 5;
+                    auto scores = [&](int kt) {
+                        float16v S = attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql);
+                        if (32 * kt + 32 > n) {
 #pragma unroll
-                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
-                }
-                mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
-                // ggml's double sum of the fp16 probabilities, exactly: every p is a
-                // multiple of 2^-24 in [0, 1], so p * 2^24 is an integer and the
-                // sum of n <= 128 of them fits a uint32
-                uint32_t sum = 0;
-                float16v o[D / 32];
+                            for (int j = 0; j < 16; j++)
+                                if (32 * kt + (j & 3) + 8 * (j >> 2) >= lim) S[j] = -INFINITY;
+                        }
+                        return S;
+                    };
+                    float mx = -INFINITY;
+                    for (int kt = 0; kt < nkt; kt++) {
+                        const float16v S = scores(kt);
 #pragma unroll
-                for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
-                for (int kt = 0; kt < nkt; kt++) {
-                    const float16v S = scores(kt);
-                    half8 ph[2];
-#pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        // ggml_scale after K.Q, then p = exp_tab[fp16(s - max)]: s - max <= 0, and
-                        // fp16(max - s) is its magnitude exactly (IEEE subtraction is sign-symmetric;
-                        // masked keys: +inf -> the constant-0 entry)
-                        const uint32_t hm = f2h(mx - S[j] * a.scale);
-                        const uint16_t pb = etab[epos + min(hm, (uint32_t)eneg)];
-                        ph[j >> 3][j & 7] = __builtin_bit_cast(_Float16, pb);
-                        sum += (uint32_t)(h2f(pb) * 16777216.0f);
+                        for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
                     }
-                    attn_pv_h<D>(o, Vh, Vl, VST, 32 * kt, r, hh, ph);
+                    mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
+                    // ggml's double sum of the fp16 probabilities, exactly: every p is a
+                    // multiple of 2^-24 in [0, 1], so p * 2^24 is an integer and the
+                    // sum of n <= 128 of them fits a uint32
+                    uint32_t sum = 0;
+                    float16v o[D / 32];
+#pragma unroll
+                    for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
+                    for (int kt = 0; kt < nkt; kt++) {
+                        const float16v S = scores(kt);
+                        half8 ph[2];
+#pragma unroll
+                        for (int j = 0; j < 16; j++) {
+                            // ggml_scale after K.Q, then p = exp_tab[fp16(s - max)]: s - max <= 0, and
+                            // fp16(max - s) is its magnitude exactly (IEEE subtraction is sign-symmetric;
+                            // masked keys: +inf -> the constant-0 entry)
+                            const uint32_t hm = f2h(mx - S[j] * a.scale);
+                            const uint16_t pb = etab[epos + min(hm, (uint32_t)eneg)];
+                            ph[j >> 3][j & 7] = __builtin_bit_cast(_Float16, pb);
+                            sum += (uint32_t)(h2f(pb) * 16777216.0f);
+                        }
+                        attn_pv_h<D>(o, Vh, Vl, VST, 32 * kt, r, hh, ph);
+                    }
+                    sum += __shfl_xor(sum, 32);
+                    attn_store_ctx<WT, D>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + q0 + r, q0 + r < n, head, hh);
                 }
-                sum += __shfl_xor(sum, 32);
-                attn_store_ctx<WT, D>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + q0 + r, q0 + r < n, head, hh);
             }
+            __syncthreads();  // the next pair's tiles / the next quad's A chunks overwrite the attention tiles
         }
-        __syncthreads();  // the next pair's A chunks overwrite the attention tiles
         QKVA_MARK(3);
     }
 }
@@ -1586,8 +1598,11 @@ static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_seqs, h
     return hipGetLastError();
 }
 
+int qkv_attention_ntw(int wtype) { return (wtype == W_Q4_0 || wtype == W_Q4_1) ? 2 : 1; }
+
 bool qkv_attention_supported(int wtype, int E, int H, int max_len) {
-    return max_len <= 128 && E / H == QKVA_D && H % 2 == 0 && E % KC == 0 && wtype != W_F32;
+    return max_len <= 128 && E / H == QKVA_D && H % (2 * qkv_attention_ntw(wtype)) == 0 && E % KC == 0 &&
+           wtype != W_F32;
 }
 
 hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {

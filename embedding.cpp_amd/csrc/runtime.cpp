@@ -167,7 +167,7 @@ struct DevMat {
 
 struct DevLayer {
     WPtr qkv, o, up, down;
-    WPtr qkv_plain;  // head-major QKV in plain tile order: qkv_attention_kernel's copy (when supported)
+    WPtr qkv_plain;  // head-major QKV in grouped, plain tile order: qkv_attention_kernel's copy (when supported)
     float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
 };
@@ -750,10 +750,18 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
         if (qkv_attention_supported(ctx->wtype, (int)E, (int)ctx->hp.n_head, 128)) {
             // undo repack's column interleave (row 32p + 2c + t <- 32p + 16t + c) so
             // that repacked tile j holds features 16j .. 16j + 15 in order
-            std::vector<const uint8_t *> plain(rows.size());
+            // after the grouped tile order (kernels.hip qkv_attention_kernel): tile
+            // G tpp q + G w + t <- n-tile w of head pair G q + t (tpp n-tiles per
+            // pair, G = pairs per main loop; G = 1 is the plain order)
+            const size_t tpp = (size_t)(6 * Dh / 16), G = (size_t)qkv_attention_ntw(ctx->wtype);
+            std::vector<const uint8_t *> quad(rows.size()), plain(rows.size());
+            for (size_t T = 0; T < rows.size() / 16; T++) {
+                const size_t src = tpp * (G * (T / (G * tpp)) + T % G) + (T % (G * tpp)) / G;
+                for (int c = 0; c < 16; c++) quad[16 * T + c] = rows[16 * src + c];
+            }
             for (size_t pr = 0; pr < rows.size() / 32; pr++)
                 for (int t = 0; t < 2; t++)
-                    for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = rows[32 * pr + 16 * t + c];
+                    for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = quad[32 * pr + 16 * t + c];
             if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E))) return false;
         }
         std::vector<const uint8_t *> up_rows = rows_of(l.i_w);
