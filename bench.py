@@ -102,7 +102,7 @@ def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
         "gemm_down_ln": M * I * act + E * I * wb + 2 * M * E * 4 + M * E * act,
         "attention": M * 3 * E * 4 + M * E * act,
         "qkv_attention": M * E * act + 3 * E * E * wb + M * E * act,
-        "embed_ln": M * 4 + M * E * (4 + act) + M * E * 3 * 4,  # f32 table rows on the device
+        "embed_ln": M * 4 + M * E * (4 + act) + M * E * 4,  # f32 word rows (pos/type tables stay cached)
         "pool_l2": M * E * 4 + B * E * 4,
     }.get(name, 0.0) if L else 0.0
 
