@@ -10,7 +10,7 @@ SRC := embedding.cpp_amd/csrc
 INC := -Iinclude -I$(SRC)
 HOST_SRCS := gguf_io.cpp quantize.cpp quantize_model.cpp synth.cpp tokenizer.cpp runtime.cpp
 HOST_OBJS := $(addprefix $(BUILD)/obj/,$(HOST_SRCS:.cpp=.o))
-HIP_OBJS := $(BUILD)/obj/kernels.o
+HIP_OBJS := $(BUILD)/obj/kernels.o $(BUILD)/obj/gemm_i8.o
 CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
 HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
@@ -23,7 +23,7 @@ $(BUILD)/obj/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/bert.h include/ber
 
 $(BUILD)/obj/tokenizer.o: $(SRC)/unicode_tables.inc
 
-$(BUILD)/obj/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.h
+$(BUILD)/obj/%.o: $(SRC)/%.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -46,3 +46,9 @@ $(BUILD)/gemm_bench: tools/gemm_bench.hip embedding.cpp_amd/csrc/kernels.hip emb
 $(BUILD)/div_check: tools/div_check.hip
 	@mkdir -p $(BUILD)
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -Wno-unused-value -Wno-unused-result $< -o $@
+
+# development timing harness for the int8-MFMA GEMMs (not shipped); I8_EXP=n compiles a timing ablation
+I8_EXP ?= 0
+$(BUILD)/i8_bench$(I8_SUFFIX): tools/i8_bench.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DI8_EXP=$(I8_EXP) $< -o $@

@@ -63,12 +63,16 @@ bool read_value(Cursor &c, uint32_t type, GGUFValue &v) {
         case GV_ARR: {
             v.arr_type = c.get<uint32_t>();
             v.arr_n = c.get<uint64_t>();
+            if (!c.ok) return false;
+            const uint64_t left = (uint64_t)(c.end - c.p);
             if (v.arr_type == GV_STR) {
+                if (v.arr_n > left / 8) return false;  // every string needs at least its 8-byte length
                 v.arr_str.reserve((size_t)v.arr_n);
                 for (uint64_t i = 0; i < v.arr_n && c.ok; i++) v.arr_str.push_back(c.str());
             } else {
                 const size_t es = scalar_size(v.arr_type);
                 if (es == 0) return false;  // nested arrays are not used by BERT GGUFs
+                if (v.arr_n > left / es) return false;  // (also keeps arr_n * es from wrapping)
                 const size_t nb = (size_t)v.arr_n * es;
                 if (!c.need(nb)) return false;
                 v.arr_raw.assign(c.p, c.p + nb);
@@ -141,14 +145,24 @@ bool GGUFFile::open(const std::string &path, std::string &err) {
         if (!read_value(c, t, v)) { err = "bad KV '" + key + "'"; return false; }
         kv.emplace_back(std::move(key), std::move(v));
     }
-    if (const GGUFValue *a = find("general.alignment")) alignment = (size_t)a->u;
-    if (alignment == 0 || (alignment & (alignment - 1))) { err = "bad alignment"; return false; }
+    if (const GGUFValue *a = find("general.alignment")) {
+        if (a->type != GV_U32) { err = "bad alignment"; return false; }
+        alignment = (size_t)a->u;
+    }
+    if (alignment == 0 || alignment > (1u << 20) || (alignment & (alignment - 1))) { err = "bad alignment"; return false; }
+    // every tensor info needs at least 8 (name) + 4 (rank) + 4 (type) + 8 (offset) bytes
+    if (n_tensors > (uint64_t)(c.end - c.p) / 24) { err = "truncated GGUF header"; return false; }
     for (uint64_t i = 0; i < n_tensors && c.ok; i++) {
         GGUFTensor t;
         t.name = c.str();
         const uint32_t nd = c.get<uint32_t>();
         if (nd > 4) { err = "tensor rank > 4"; return false; }
-        for (uint32_t d = 0; d < nd; d++) t.ne.push_back((int64_t)c.get<uint64_t>());
+        for (uint32_t d = 0; d < nd; d++) {
+            const uint64_t ne = c.get<uint64_t>();
+            // ne >= 1 and < 2^31 per dimension: the row product below cannot wrap
+            if (c.ok && (ne == 0 || ne >= (1ull << 31))) { err = "bad tensor shape: " + t.name; return false; }
+            t.ne.push_back((int64_t)ne);
+        }
         t.type = c.get<uint32_t>();
         t.offset = c.get<uint64_t>();
         tensors.push_back(std::move(t));
@@ -156,12 +170,28 @@ bool GGUFFile::open(const std::string &path, std::string &err) {
     if (!c.ok) { err = "truncated GGUF header"; return false; }
     size_t data_off = (size_t)(c.p - (const uint8_t *)map_);
     data_off = (data_off + alignment - 1) / alignment * alignment;
+    if (data_off > map_size_) { err = "truncated GGUF file"; return false; }
+    const size_t data_size = map_size_ - data_off;
     for (auto &t : tensors) {
-        int64_t ne0 = t.ne.empty() ? 1 : t.ne[0];
+        const int64_t ne0 = t.ne.empty() ? 1 : t.ne[0];
         const size_t rb = ggml_row_bytes(t.type, ne0);
         if (rb == 0) { err = "unsupported tensor type " + std::to_string(t.type) + " for " + t.name; return false; }
-        t.nbytes = rb * (size_t)t.nrows();
-        if (data_off + t.offset + t.nbytes > map_size_) { err = "tensor data out of range: " + t.name; return false; }
+        if ((t.type == GT_Q4_0 || t.type == GT_Q4_1 || t.type == GT_Q8_0 || t.type == GT_Q8_1) && ne0 % QK) {
+            err = "row length not a multiple of the block size: " + t.name;
+            return false;
+        }
+        // nrows <= data_size / rb, checked dimension by dimension (no overflow)
+        uint64_t rows = 1;
+        const uint64_t max_rows = data_size / rb;
+        for (size_t d = 1; d < t.ne.size(); d++) {
+            if ((uint64_t)t.ne[d] > max_rows / rows) { err = "tensor data out of range: " + t.name; return false; }
+            rows *= (uint64_t)t.ne[d];
+        }
+        t.nbytes = rb * (size_t)rows;
+        if (t.offset > data_size || t.nbytes > data_size - t.offset) {
+            err = "tensor data out of range: " + t.name;
+            return false;
+        }
         t.data = (const uint8_t *)map_ + data_off + t.offset;
     }
     return true;

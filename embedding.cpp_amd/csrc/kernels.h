@@ -50,6 +50,22 @@ struct WPtr {
     float unscale = 1.f;
 };
 
+// Q4_0 / Q4_1 weights for the int8-MFMA GEMMs (gemm_i8.hip), repacked at load
+// (runtime.cpp repack_i8) per 32-row f-tile ft and 32-wide k block b:
+//   q: int8 [N/32][K/32][64][16]: lane (m = l & 31, h = l >> 5) byte j holds
+//      q - 8 (Q4_0) or q (Q4_1) of weight row 32 ft + perm(m), k = 32 b + 16 h + j,
+//      perm(m) = 16 ((m >> 2) & 1) + 4 (m >> 3) + (m & 3) (so that a lane of the
+//      32x32 MFMA result holds 16 consecutive output features)
+//   d: f32 [N/32][K/128][32][4]: d_w of row 32 ft + perm(m), blocks 4g .. 4g + 3
+//   m: Q4_1's m_w, same layout (null for Q4_0)
+//   dh: Q4_0: the fp16 d_w themselves, fp16 [N/32][K/128][32][4] (the f16-MFMA scale operand)
+struct I8W {
+    const int8_t *q = nullptr;
+    const float *d = nullptr;
+    const float *m = nullptr;
+    const uint16_t *dh = nullptr;
+};
+
 enum Epi : int {
     EPI_QKV = 0,       // y = b + W.x split hi/lo for attention (Q|K row-major, V transposed)
     EPI_GELU_ACT = 1,  // gelu(b + W.x) in the next matmul's activation format
@@ -81,6 +97,7 @@ struct GemmArgs {
     ActPtr A;              // [Mpad][K] in the activation format of wtype
     int K = 0;
     WPtr W;                // [N][K] repacked
+    I8W Wi;                // the same weights for the int8 path (Q4 GEMMs in gemm_i8.hip)
     int N = 0;
     const float *bias = nullptr;   // [N]
     // EPI_QKV: y = b + W.x (f32, as ggml), stored split for the attention MFMAs:
@@ -144,5 +161,10 @@ bool gemm_ln_fused(int wtype, int N);  // false: EPI_RESID + launch_ln
 // tile 2p + t, fragment row r <- weight row 32p + 8(r >> 2) + 4t + (r & 3)), so
 // the transposed accumulators give each lane 8 adjacent columns of one row
 bool gemm_gelu_blk8(int wtype);
+
+// Q4 x Q8 GEMMs on the int8 MFMA (gemm_i8.hip): EPI_GELU_ACT (N % 256 == 0),
+// EPI_LN (N == 384), EPI_RESID (N % 256 == 0); K % 128 == 0; Mpad % 128 == 0.
+bool i8_gemm_supported(int epi, int N, int K);
+hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
 
 }  // namespace bertamd

@@ -167,6 +167,7 @@ struct DevMat {
 
 struct DevLayer {
     WPtr qkv, o, up, down;
+    I8W o8, up8, down8;  // Q4 weights for the int8-MFMA GEMMs (gemm_i8.hip)
     WPtr qkv_plain;  // head-major QKV in grouped, plain tile order: qkv_attention_kernel's copy (when supported)
     float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
@@ -228,6 +229,7 @@ struct bert_ctx {
     int32_t cls_id = 101, sep_id = 102, pad_id = 0;
     WordPieceTokenizer tokenizer;
     std::vector<std::unique_ptr<Replica>> reps;
+    bool i8 = false;  // O / FFN projections on the int8-MFMA GEMMs (use_i8)
     std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
 };
 
@@ -340,6 +342,59 @@ Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_
     return p;
 }
 
+// Repack a Q4_0 / Q4_1 [N][K] matrix for the int8-MFMA GEMMs (kernels.h
+// I8W): nibbles expanded to int8 (q - 8 for Q4_0, q for Q4_1) in fragment
+// order, the fp16 block scales (and Q4_1 minima) widened to f32 vectors.
+// Weight row m of each 32-row tile holds feature perm(m), so that a lane of
+// the 32x32 MFMA result holds 16 consecutive output features.
+bool upload_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vector<const uint8_t *> &rows,
+               int64_t K) {
+    const int64_t N = (int64_t)rows.size(), nkb = K / 32, nft = N / 32;
+    const bool q1 = type == GT_Q4_1;
+    const int bs = q1 ? 20 : 18, qoff = q1 ? 4 : 2;
+    auto perm = [](int m) { return 16 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3); };
+    std::vector<int8_t> q((size_t)(N * K));
+    std::vector<float> d((size_t)(N * nkb)), mv(q1 ? (size_t)(N * nkb) : 0);
+    std::vector<uint16_t> dhv(q1 ? 0 : (size_t)(N * nkb));
+    for (int64_t ft = 0; ft < nft; ft++)
+        for (int64_t b = 0; b < nkb; b++)
+            for (int lane = 0; lane < 64; lane++) {
+                const int mrow = lane & 31, h = lane >> 5;
+                const uint8_t *blk = rows[(size_t)(32 * ft + perm(mrow))] + b * bs;
+                int8_t *dst = &q[(size_t)(((ft * nkb + b) * 64 + lane) * 16)];
+                for (int j = 0; j < 16; j++) {
+                    const int e = 16 * h + j;
+                    const uint8_t byte = blk[qoff + (e & 15)];
+                    const int v = e < 16 ? (byte & 15) : (byte >> 4);
+                    dst[j] = (int8_t)(q1 ? v : v - 8);
+                }
+            }
+    for (int64_t ft = 0; ft < nft; ft++)
+        for (int64_t g = 0; g < nkb / 4; g++)
+            for (int mrow = 0; mrow < 32; mrow++)
+                for (int jj = 0; jj < 4; jj++) {
+                    const uint8_t *blk = rows[(size_t)(32 * ft + perm(mrow))] + (4 * g + jj) * bs;
+                    uint16_t dh, mh;
+                    std::memcpy(&dh, blk, 2);
+                    const size_t at = (size_t)(((ft * (nkb / 4) + g) * 32 + mrow) * 4 + jj);
+                    d[at] = f16_to_f32(dh);
+                    if (!q1) dhv[at] = dh;
+                    if (q1) {
+                        std::memcpy(&mh, blk + 2, 2);
+                        mv[at] = f16_to_f32(mh);
+                    }
+                }
+    void *pq = nullptr, *pd = nullptr, *pm = nullptr, *ph = nullptr;
+    if (!upload(track, &pq, q.data(), q.size()) || !upload(track, &pd, d.data(), d.size() * 4)) return false;
+    if (q1 && !upload(track, &pm, mv.data(), mv.size() * 4)) return false;
+    if (!q1 && !upload(track, &ph, dhv.data(), dhv.size() * 2)) return false;
+    w.q = (const int8_t *)pq;
+    w.d = (const float *)pd;
+    w.m = (const float *)pm;
+    w.dh = (const uint16_t *)ph;
+    return true;
+}
+
 bool upload_packed(std::vector<void *> &track, WPtr &w, const Packed &p) {
     void *q = nullptr;
     if (!upload(track, &q, p.q.data(), p.q.size())) return false;
@@ -446,6 +501,21 @@ void drain_profile(Replica &R) {
         }                                                                                 \
     } while (0)
 
+// Q4 models can run the O / FFN projections on the int8-MFMA GEMMs
+// (gemm_i8.hip: in-kernel scale application, 1 B/weight, one isum MFMA per
+// block).  Opt-in (env BERT_AMD_I8=1, read at load): on MI355X they measure
+// slower than the split-fp16 GEMMs today, so the default keeps
+// the split-fp16 path.
+bool use_i8(const bert_ctx *ctx) { return ctx->i8; }
+
+bool i8_wanted(const bert_ctx *ctx) {
+    const char *e = std::getenv("BERT_AMD_I8");
+    const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
+    return e && *e && *e != '0' && (ctx->wtype == W_Q4_0 || ctx->wtype == W_Q4_1) &&
+           i8_gemm_supported(EPI_GELU_ACT, I, E) && i8_gemm_supported(E == 384 ? EPI_LN : EPI_RESID, E, I) &&
+           i8_gemm_supported(E == 384 ? EPI_LN : EPI_RESID, E, E);
+}
+
 // One encoder layer over the row group [row0, row0 + rows) (sentences
 // d_off[0 .. nseq), absolute row offsets).  Xa / Ca / Ua / X point at the
 // group's first row; the QKV + attention kernels index rows absolutely through
@@ -507,7 +577,16 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
         o.ln_w = L.ln1_w;
         o.ln_b = L.ln1_b;
         o.eps = hp.eps;
-        if (ln_fused) {
+        const bool i8 = use_i8(ctx);
+        if (i8) {
+            o.Wi = L.o8;
+            if (E == 384) {
+                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt, EPI_LN, o, (int)rows, st));
+            } else {
+                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt, EPI_RESID, o, (int)rows, st));
+                LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
+            }
+        } else if (ln_fused) {
             LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)rows, st));
@@ -524,7 +603,12 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
         u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
         u.gelu.n_pad = (int)tables().gelu_pair.size();  // the pair view (kernels.hip gelu_lookup)
         u.gelu.cap = tables().gelu_cap;
-        LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)rows, st));
+        if (i8) {
+            u.Wi = L.up8;
+            LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt, EPI_GELU_ACT, u, (int)rows, st));
+        } else {
+            LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)rows, st));
+        }
 
         GemmArgs dn;
         dn.A = Ua;
@@ -537,7 +621,15 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
         dn.ln_w = L.ln2_w;
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
-        if (ln_fused) {
+        if (i8) {
+            dn.Wi = L.down8;
+            if (E == 384) {
+                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt, EPI_LN, dn, (int)rows, st));
+            } else {
+                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt, EPI_RESID, dn, (int)rows, st));
+                LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
+            }
+        } else if (ln_fused) {
             LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)rows, st));
@@ -774,10 +866,16 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                 for (int t = 0; t < 2; t++)
                     for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
         }
-        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E)) || !upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E)) ||
-            !upload_packed(tr, dl.up, repack(wt, up_rows, E)) ||
-            !upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I)))
+        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
+        if (use_i8(ctx)) {
+            if (!upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) || !upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) ||
+                !upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I))
+                return false;
+        } else if (!upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E)) ||
+                   !upload_packed(tr, dl.up, repack(wt, up_rows, E)) ||
+                   !upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))) {
             return false;
+        }
         if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
             !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||
             !upload(tr, &dl.ln1_w, l.ln1_w->data, E * 4) || !upload(tr, &dl.ln1_b, l.ln1_b->data, E * 4) ||
@@ -861,6 +959,13 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
         return nullptr;
     }
     hp.eps = (float)eps->f;
+    // header sanity before anything indexes layers or divides by the head count
+    if (hp.n_layer <= 0 || hp.n_layer > 1024 || hp.n_head <= 0 || hp.n_embd <= 0 || hp.n_embd % hp.n_head ||
+        hp.n_intermediate <= 0 || hp.n_max_tokens <= 0 || hp.n_vocab <= 0) {
+        set_err("invalid hparams: n_vocab=%d n_max_tokens=%d n_embd=%d n_intermediate=%d n_head=%d n_layer=%d",
+                hp.n_vocab, hp.n_max_tokens, hp.n_embd, hp.n_intermediate, hp.n_head, hp.n_layer);
+        return nullptr;
+    }
     // tokenizer (reference bert.cpp:515-578)
     if (!f.find("tokenizer.ggml.scores")) { set_err("cannot find tokenizer scores in model file"); return nullptr; }
     if (!f.find("tokenizer.ggml.token_type")) { set_err("cannot find token type list in GGUF file"); return nullptr; }
@@ -940,6 +1045,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
                 tables().gelu_pair.size(), tables().exp_c.compact.size());
         return nullptr;
     }
+    ctx->i8 = i8_wanted(ctx.get());
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {

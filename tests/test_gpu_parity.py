@@ -90,6 +90,28 @@ def test_every_weight_type_vs_oracle(ftype, model_dir):
     assert c.min() >= COS_TOL, (ftype, 1 - c)
 
 
+@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_1", "minilm_q4_0_std01"])
+def test_int8_gemm_path_golden(case, model_dir, monkeypatch):
+    """The opt-in int8-MFMA Q4 GEMMs (env BERT_AMD_I8=1: gemm_i8.hip, scales
+    applied in-kernel per block like ggml_vec_dot_q4_x_q8_x) against the same
+    golden fixtures, and bitwise deterministic."""
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    monkeypatch.setenv("BERT_AMD_I8", "1")
+    m = bertlib.BertModel(p)
+    try:
+        got = m.eval_batch(toks)
+        assert np.array_equal(got, m.eval_batch(toks))
+    finally:
+        m.close()
+    c = cos(got, want)
+    print(f"int8 {case}: 1-cos max {1 - c.min():.2e}")
+    if case in CHAOTIC:
+        assert np.all(1 - c <= np.maximum(2.0 * np.asarray(meta["exact_restatement_1mcos"]), 1 - COS_TOL))
+    else:
+        assert c.min() >= COS_TOL, (case, 1 - c)
+
+
 def test_batch_invariance_and_determinism(model_dir):
     p, m = get_model(model_dir, "minilm", "q4_0")
     toks = [sentence(i, n, 30522) for i, n in enumerate([5, 128, 64, 17, 512, 128])]
