@@ -15,7 +15,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wn
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
 HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
 
-all: $(BUILD)/libbert.so $(BUILD)/div_check
+all: $(BUILD)/libbert.so $(BUILD)/div_check $(BUILD)/qkva_check
 
 $(BUILD)/obj/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/bert.h include/bert_amd.h
 	@mkdir -p $(dir $@)
@@ -52,3 +52,8 @@ I8_EXP ?= 0
 $(BUILD)/i8_bench$(I8_SUFFIX): tools/i8_bench.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DI8_EXP=$(I8_EXP) $< -o $@
+
+# development check of the fused kernel's head-pair grouping, F16 (tools/qkva_check.hip)
+$(BUILD)/qkva_check: tools/qkva_check.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $< -o $@

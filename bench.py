@@ -183,7 +183,17 @@ def main():
     while not os.path.exists(path):  # other nodes' local rank 0 (single node: already there)
         time.sleep(0.1)
 
-    model = bertlib.BertModel(path, devices=[local_rank])
+    # the library reports the load on stdout (as the reference's bert_load_from_file
+    # does); keep stdout for the one JSON line
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        model = bertlib.BertModel(path, devices=[local_rank])
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
     B, N = args.batch, args.seq
     first = shard(rank, B)
     toks = splitmix_tokens(first, B, N, hp["n_vocab"])

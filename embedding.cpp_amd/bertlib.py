@@ -34,7 +34,7 @@ ABI_SYMBOLS = [
 EXT_SYMBOLS = [
     "bert_amd_load", "bert_amd_n_devices", "bert_amd_hparams", "bert_amd_eval_device",
     "bert_amd_profile_enable", "bert_amd_profile_read", "bert_amd_synth_model", "bert_amd_tokenize_json",
-    "bert_amd_last_error",
+    "bert_amd_workspace_rows", "bert_amd_last_error",
 ]
 
 # model shapes of BASELINE.json's configs
@@ -92,6 +92,8 @@ def lib() -> ctypes.CDLL:
     L.bert_amd_tokenize_json.restype = ctypes.c_int32
     L.bert_amd_tokenize_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, I_P, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+    L.bert_amd_workspace_rows.restype = ctypes.c_int64
+    L.bert_amd_workspace_rows.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     L.bert_amd_last_error.restype = ctypes.c_char_p
     _lib = L
     return L
@@ -204,6 +206,9 @@ class BertModel:
                                            ctypes.c_void_p(d_out_ptr), ctypes.c_void_p(stream or None))
         if rc != 0:
             raise RuntimeError(f"bert_amd_eval_device failed ({rc}): {last_error()}")
+
+    def workspace_rows(self, slot: int = 0) -> int:
+        return int(self.lib.bert_amd_workspace_rows(self.ctx, slot))
 
     def profile(self, enable: bool) -> None:
         self.lib.bert_amd_profile_enable(self.ctx, 1 if enable else 0)

@@ -5,13 +5,15 @@
 // the ggml semantics restated in SURVEY.md Appendix A wherever they are cheap
 // to reproduce exactly (Q8 activation quantisation, fp16 GELU/exp tables,
 // double-accumulated LayerNorm and softmax sums, fp16 activation rounding);
-// the weight GEMMs run on fp16 MFMA with the Q4 weights dequantised in
-// registers (DESIGN.md §3-4 for the precision argument).
+// the weight GEMMs run on fp16 MFMA; Q4 weights are expanded once at load
+// into exact fp16 hi/lo pairs of d_w * q (runtime.cpp repack), so the
+// kernels apply only the activation scale d_a per block.
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
 #include "kernels_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace bertamd {
 
@@ -1239,7 +1241,7 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 // n <= 128 tokens and heads of D = 32 (MiniLM): one 12-wave workgroup per
 // sentence, so Q, K and V (hi/lo, 4 bytes a value) never leave the CU —
 // the unfused pair writes and re-reads 12 bytes per token and feature.
-// Heads go four at a time (Q4; two for F16) through the GEMM main loop (one
+// Heads go four at a time (qkv_attention_ntw) through the GEMM main loop (one
 // n-tile per wave and head pair) and two at a time through the attention tiles: the main loop (gemm_mainloop, the 128 rows
 // from the sentence's first token) computes the pair's 192 head-major QKV
 // features (kernels.h GemmArgs), one 16-feature n-tile per wave; b + W.x is
@@ -1260,11 +1262,10 @@ __device__ unsigned long long qkva_prof[4];
 #define QKVA_MARK(i) do {} while (0)
 #endif
 
-template <int WT>
+template <int WT, int NTW>  // NTW: head pairs per main loop (qkv_attention_ntw)
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
     constexpr int D = QKVA_D, NW = QKVA_NW, BM = 128, RT = BM / 16;
-    constexpr int NTW = QP ? 2 : 1;  // head pairs per main loop (qkv_attention_ntw)
     constexpr int NK = 128, KST = D + 8, VST = NK + 4;
     constexpr int A_BUF = (WT == W_F32 ? BM * LDA_F * 4 : BM * LDA_H * 2) + (QP ? KB * BM * 4 : 0);
     constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
@@ -1301,8 +1302,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
         // heads 2 NTW qd ..: one main loop (one pass over the sentence's A panel)
         // serves NTW head pairs.  g.W is in grouped tile order (runtime.cpp): wave
         // w's n-tiles nt0 + t are n-tile w of pair NTW qd + t, so acc[..][half]
-        // plays the one-pair role of the split below.  (NTW = 2 for F16 measured
-        // 28 % faster but fails parity, DESIGN.md §3: F16 stays at one pair.)
+        // plays the one-pair role of the split below.
         const int64_t nt0 = (int64_t)qd * NTW * NW + NTW * wv;
         float4v acc[RT][NTW];
         QKVA_MARK(0);
@@ -1430,11 +1430,24 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 
 template <int WT>
 static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
-    hipLaunchKernelGGL((qkv_attention_kernel<WT>), dim3(n_seqs), dim3(QKVA_NW * 64), 0, s, g, a);
+    if (qkv_attention_ntw(WT) == 2)
+        hipLaunchKernelGGL((qkv_attention_kernel<WT, 2>), dim3(n_seqs), dim3(QKVA_NW * 64), 0, s, g, a);
+    else
+        hipLaunchKernelGGL((qkv_attention_kernel<WT, 1>), dim3(n_seqs), dim3(QKVA_NW * 64), 0, s, g, a);
     return hipGetLastError();
 }
 
-int qkv_attention_ntw(int wtype) { return (wtype == W_Q4_0 || wtype == W_Q4_1) ? 2 : 1; }
+// Head pairs per main loop: two (one pass over a sentence's A panel serves
+// four heads).  Env BERT_AMD_QKVA_NTW=1 selects one pair per pass (A/B
+// checks; tools/qkva_check.hip compares the two bitwise).
+int qkv_attention_ntw(int wtype) {
+    (void)wtype;
+    static const int ntw = [] {
+        const char *e = std::getenv("BERT_AMD_QKVA_NTW");
+        return e && std::atoi(e) == 1 ? 1 : 2;
+    }();
+    return ntw;
+}
 
 bool qkv_attention_supported(int wtype, int E, int H, int max_len) {
     return max_len <= 128 && E / H == QKVA_D && H % (2 * qkv_attention_ntw(wtype)) == 0 && E % KC == 0 &&

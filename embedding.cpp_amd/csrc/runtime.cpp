@@ -427,13 +427,24 @@ bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, i
     return true;
 }
 
-bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs) {
+// Grows the workspace to Mpad rows / n_seqs sentences.  The old buffers may
+// still be in use on any stream of the device (the library's or a caller's),
+// so the device is drained before they are freed; the zero-fill of the new
+// ones is issued on `st`, the stream the kernels that use them run on.
+bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, hipStream_t st) {
     Workspace &w = R.ws;
     if (Mpad <= w.cap_rows && n_seqs <= w.cap_seqs) return true;
-    HIP_OK(hipStreamSynchronize(R.stream));
+    HIP_OK(hipDeviceSynchronize());
+    const int64_t rows = std::max<int64_t>(Mpad, w.cap_rows), seqs = std::max<int64_t>(n_seqs, w.cap_seqs);
     for (void *p : w.allocs) hipFree(p);
     w.allocs.clear();
-    const int64_t rows = std::max<int64_t>(Mpad, w.cap_rows), seqs = std::max<int64_t>(n_seqs, w.cap_seqs);
+    // until every allocation below has succeeded the workspace is empty
+    // (a failed grow must not leave capacities that point at freed memory)
+    w.cap_rows = w.cap_seqs = 0;
+    w.X = w.out = nullptr;
+    w.qk_hi = w.qk_lo = w.vt_hi = w.vt_lo = nullptr;
+    w.Xa = w.Ca = w.Ua = ActPtr{};
+    w.tok = w.off = w.rowpos = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const int wt = ctx->wtype;
     if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
@@ -445,11 +456,11 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs) {
         !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4))
         return false;
     // padding rows must hold finite values: zero everything once
-    HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, R.stream));
-    HIP_OK(hipMemsetAsync(w.qk_hi, 0, (size_t)rows * 2 * E * 2, R.stream));
-    HIP_OK(hipMemsetAsync(w.qk_lo, 0, (size_t)rows * 2 * E * 2, R.stream));
-    HIP_OK(hipMemsetAsync(w.vt_hi, 0, (size_t)rows * E * 2, R.stream));
-    HIP_OK(hipMemsetAsync(w.vt_lo, 0, (size_t)rows * E * 2, R.stream));
+    HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, st));
+    HIP_OK(hipMemsetAsync(w.qk_hi, 0, (size_t)rows * 2 * E * 2, st));
+    HIP_OK(hipMemsetAsync(w.qk_lo, 0, (size_t)rows * 2 * E * 2, st));
+    HIP_OK(hipMemsetAsync(w.vt_hi, 0, (size_t)rows * E * 2, st));
+    HIP_OK(hipMemsetAsync(w.vt_lo, 0, (size_t)rows * E * 2, st));
     w.cap_rows = rows;
     w.cap_seqs = seqs;
     return true;
@@ -647,7 +658,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
     int max_len = 0;
     for (int s = 0; s < n_seqs; s++) max_len = std::max(max_len, h_off[s + 1] - h_off[s]);
-    if (!ensure_workspace(ctx, R, Mpad, n_seqs)) return false;
+    if (!ensure_workspace(ctx, R, Mpad, n_seqs, st)) return false;
     Workspace &w = R.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, wt = ctx->wtype;
     const bool ln_fused = gemm_ln_fused(wt, E);
@@ -1077,9 +1088,12 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
 }
 
 bool grow_pinned(Workspace &w, int64_t rows, int64_t seqs, int64_t E) {
+    // callers hold ctx->mu and the replica's previous copies have completed
+    // (eval_host_slice synchronises its stream), so the old buffers are idle
     if (rows > w.h_cap_rows) {
         if (w.h_tok) hipHostFree(w.h_tok);
         w.h_tok = nullptr;
+        w.h_cap_rows = 0;
         HIP_OK(hipHostMalloc((void **)&w.h_tok, (size_t)rows * 4, hipHostMallocDefault));
         w.h_cap_rows = rows;
     }
@@ -1088,6 +1102,7 @@ bool grow_pinned(Workspace &w, int64_t rows, int64_t seqs, int64_t E) {
         if (w.h_out) hipHostFree(w.h_out);
         w.h_off = nullptr;
         w.h_out = nullptr;
+        w.h_cap_seqs = 0;
         HIP_OK(hipHostMalloc((void **)&w.h_off, (size_t)(seqs + 1) * 4, hipHostMallocDefault));
         HIP_OK(hipHostMalloc((void **)&w.h_out, (size_t)seqs * E * 4, hipHostMallocDefault));
         w.h_cap_seqs = seqs;
@@ -1114,8 +1129,8 @@ bool eval_host_slice(bert_ctx *ctx, Replica &R, bert_vocab_id **toks, const int3
     }
     w.h_off[n] = (int32_t)pos;
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
-    if (!ensure_workspace(ctx, R, Mpad, n)) return false;
     const hipStream_t st = R.stream;
+    if (!ensure_workspace(ctx, R, Mpad, n, st)) return false;
     HIP_OK(hipMemcpyAsync(w.tok, w.h_tok, (size_t)M * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(w.off, w.h_off, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
     if (!run_pipeline(ctx, R, w.tok, w.off, w.h_off, n, w.out, st)) return false;
@@ -1126,6 +1141,8 @@ bool eval_host_slice(bert_ctx *ctx, Replica &R, bert_vocab_id **toks, const int3
     for (int s = s0; s < s1; s++) std::memcpy(embs[s], w.h_out + (size_t)(s - s0) * E, (size_t)E * 4);
     return true;
 }
+
+void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs);
 
 // Host-pointer batch eval, sharded over the context's replicas by token count.
 void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
@@ -1146,6 +1163,35 @@ void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *nt
             }
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
+    // A batch whose sentences all fit one 128-row tile runs the fused QKV +
+    // attention kernel; a mixed batch is evaluated as two ragged batches
+    // (short sentences, then the rest), so one long sentence does not move
+    // every short one onto the unfused pair.  Sentences are independent, so
+    // the results do not depend on the grouping.
+    const HParams &hp = ctx->hp;
+    if (qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, GEMM_BM)) {
+        std::vector<int> shrt, lng;
+        for (int s = 0; s < n; s++) (ntok[s] <= GEMM_BM ? shrt : lng).push_back(s);
+        if (!shrt.empty() && !lng.empty()) {
+            for (const std::vector<int> *grp : {&shrt, &lng}) {
+                std::vector<bert_vocab_id *> t;
+                std::vector<int32_t> c;
+                std::vector<float *> e;
+                for (int s : *grp) {
+                    t.push_back(toks[s]);
+                    c.push_back(ntok[s]);
+                    e.push_back(embs[s]);
+                }
+                dispatch_batch(ctx, (int32_t)grp->size(), t.data(), c.data(), e.data());
+            }
+            return;
+        }
+    }
+    dispatch_batch(ctx, n, toks, ntok, embs);
+}
+
+// Shards one ragged batch over the context's replicas (caller holds ctx->mu).
+void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
     const int nr = (int)ctx->reps.size();
     // contiguous slices balanced by token count
     std::vector<int> cut(nr + 1, n);
@@ -1281,9 +1327,13 @@ void bert_encode(bert_ctx *ctx, int32_t n_threads, const char *texts, float *emb
 
 void bert_encode_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, int32_t n_inputs, const char **texts,
                        float **embeddings) {
-    // reference bert.cpp:1119-1198 tokenises everything, sorts by length and
-    // evaluates one sentence at a time; here the whole set is one ragged
-    // batch (n_batch_size only bounds the per-call working set).
+    // reference bert.cpp:1119-1198: tokenise everything, sort by token count
+    // (std::sort on the lengths, :1176-1177), evaluate in slices of
+    // n_batch_size (the reference forces the slice to 1, :1128; here each
+    // slice is one ragged GPU batch).  n_batch_size bounds the per-call
+    // working set (device workspace and pinned staging grow to the largest
+    // slice); n_batch_size <= 0 means all inputs in one slice.  Sorting makes
+    // each slice's lengths similar, so padding and tile waste stay small.
     if (!ctx || n_inputs <= 0 || !texts || !embeddings) return;
     const int32_t N = ctx->hp.n_max_tokens;
     std::vector<bert_vocab_id> buf((size_t)N * n_inputs);
@@ -1295,10 +1345,21 @@ void bert_encode_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, i
         bert_tokenize(ctx, texts[i], ids, &ntok[i], N);
         ids += ntok[i];
     }
-    const int32_t chunk = std::max<int32_t>(n_inputs, std::max<int32_t>(n_batch_size, 1));
+    std::vector<int> idx(n_inputs);
+    for (int i = 0; i < n_inputs; i++) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return ntok[a] < ntok[b]; });
+    std::vector<bert_vocab_id *> sp(n_inputs);
+    std::vector<int32_t> sn(n_inputs);
+    std::vector<float *> se(n_inputs);
+    for (int i = 0; i < n_inputs; i++) {
+        sp[i] = ptr[idx[i]];
+        sn[i] = ntok[idx[i]];
+        se[i] = embeddings[idx[i]];
+    }
+    const int32_t chunk = n_batch_size > 0 ? std::min(n_batch_size, n_inputs) : n_inputs;
     for (int32_t i = 0; i < n_inputs; i += chunk) {
         const int32_t m = std::min(chunk, n_inputs - i);
-        bert_eval_batch(ctx, n_threads, m, ptr.data() + i, ntok.data() + i, embeddings + i);
+        bert_eval_batch(ctx, n_threads, m, sp.data() + i, sn.data() + i, se.data() + i);
     }
 }
 
@@ -1346,8 +1407,13 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
         }
     }
     Replica &R = *ctx->reps[slot];
+    // one eval at a time per context: the workspace and the profiling state
+    // are shared with bert_eval_batch and the profile_* calls
+    std::lock_guard<std::mutex> lk(ctx->mu);
     if (hipSetDevice(R.device) != hipSuccess) { set_err("hipSetDevice failed"); return -3; }
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : R.stream;
+    // the caller's stream, as given: NULL is HIP's null (legacy default)
+    // stream, which is ordered with the caller's other work on it
+    const hipStream_t st = (hipStream_t)hip_stream;
     try {
         if (!run_pipeline(ctx, R, d_tokens, d_offsets, h_offsets, n_seqs, d_out, st)) return -4;
     } catch (const std::exception &e) {
@@ -1359,6 +1425,7 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
 
 int32_t bert_amd_profile_enable(bert_ctx *ctx, int32_t enable) {
     if (!ctx) return -1;
+    std::lock_guard<std::mutex> lk(ctx->mu);
     for (auto &r : ctx->reps) {
         hipSetDevice(r->device);
         hipDeviceSynchronize();
@@ -1372,6 +1439,7 @@ int32_t bert_amd_profile_enable(bert_ctx *ctx, int32_t enable) {
 int32_t bert_amd_profile_read(bert_ctx *ctx, char *names_buf, int32_t names_len, float *total_ms, int32_t *counts,
                               int32_t max_entries) {
     if (!ctx) return -1;
+    std::lock_guard<std::mutex> lk(ctx->mu);
     std::map<std::string, ProfEntry> agg;
     for (auto &r : ctx->reps) {
         hipSetDevice(r->device);
@@ -1395,6 +1463,12 @@ int32_t bert_amd_profile_read(bert_ctx *ctx, char *names_buf, int32_t names_len,
         i++;
     }
     return i;
+}
+
+int64_t bert_amd_workspace_rows(bert_ctx *ctx, int32_t slot) {
+    if (!ctx || slot < 0 || slot >= (int32_t)ctx->reps.size()) return -1;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return ctx->reps[slot]->ws.cap_rows;
 }
 
 const char *bert_amd_last_error(void) { return g_err.c_str(); }

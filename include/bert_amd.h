@@ -35,9 +35,10 @@ BERT_API int32_t bert_amd_n_devices(struct bert_ctx *ctx);
 BERT_API int32_t bert_amd_hparams(struct bert_ctx *ctx, int32_t *out7);
 
 /* Device-resident evaluation on replica `slot` (index into the context's
-   device list), enqueued on `hip_stream` (a hipStream_t; NULL = the
-   library's own stream for that device).  Asynchronous: returns after
-   enqueueing.
+   device list), enqueued on `hip_stream` (a hipStream_t; NULL = HIP's null
+   stream, i.e. torch's default stream).  Asynchronous: returns after
+   enqueueing; every kernel and workspace fill runs on `hip_stream`.  Takes
+   the context's lock (one eval at a time per context, like bert_eval_batch).
      d_tokens   : int32, packed token ids of all sentences (device memory)
      d_offsets  : int32[n_seqs+1], prefix offsets into d_tokens (device memory)
      h_offsets  : the same offsets in host memory (used for grid sizing)
@@ -70,6 +71,11 @@ BERT_API int bert_amd_synth_model(const char *path, int32_t n_vocab, int32_t n_m
 BERT_API int32_t bert_amd_tokenize_json(const char *tokenizer_json, const char *text, int32_t *tokens,
                                         int32_t n_max_tokens, int32_t frame, int32_t cls_id, int32_t sep_id,
                                         int32_t pad_id);
+
+/* Rows (tokens, padded to the 128-row tile) the device workspace of replica
+   `slot` currently holds; -1 on a bad argument.  Lets callers and tests see
+   that bert_encode_batch's n_batch_size bounds the working set. */
+BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
 
 BERT_API const char *bert_amd_last_error(void);
 

@@ -284,8 +284,49 @@ void oracle_quantize_q8(const float *x, int64_t k, int is_q8_1, float *d_out, fl
     }
 }
 
+/* Summation order of the dot kernels.  ggml computes the same products in a
+   different f32 order per build; every order below is one a ggml@8ca2c19
+   build of the reference runs (ggml.c: the AVX2 branch, the plain-C fallback
+   after the SIMD #if chain, and the AVX-512 register width), so the spread
+   between them measures how sensitive a model/input is to f32-level
+   reassociation — the bound any non-ggml implementation can be held to
+   (tests/golden/make_golden.py).
+     0: AVX2 (the default checker)        1: plain C (generic fallback)
+     2: 16-lane (AVX-512 register width) */
+static int g_dot_variant = 0;
+void oracle_set_dot_variant(int v) { g_dot_variant = v; }
+
+static float dot_f32_generic(int n, const float *x, const float *y) {
+    double sumf = 0.0; /* ggml_float */
+    for (int i = 0; i < n; i++) sumf += (double)(x[i] * y[i]);
+    return (float)sumf;
+}
+static float dot_f16_generic(int n, const uint16_t *x, const uint16_t *y) {
+    double sumf = 0.0;
+    for (int i = 0; i < n; i++) sumf += (double)(F16(x[i]) * F16(y[i]));
+    return (float)sumf;
+}
+/* 16 lanes: one accumulator per lane, then 16 -> 8 -> the AVX2 hsum tail */
+static float dot_f32_16(int n, const float *x, const float *y, int half) {
+    float acc[16] = {0};
+    int np = n & ~15;
+    for (int i = 0; i < np; i += 16)
+        for (int l = 0; l < 16; l++)
+            acc[l] = fmaf(half ? F16(((const uint16_t *)x)[i + l]) : x[i + l],
+                          half ? F16(((const uint16_t *)y)[i + l]) : y[i + l], acc[l]);
+    for (int l = 0; l < 8; l++) acc[l] += acc[l + 8];
+    float r4[4];
+    for (int l = 0; l < 4; l++) r4[l] = acc[l + 4] + acc[l];
+    float sumf = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+    for (int i = np; i < n; i++)
+        sumf = fmaf(half ? F16(((const uint16_t *)x)[i]) : x[i], half ? F16(((const uint16_t *)y)[i]) : y[i], sumf);
+    return sumf;
+}
+
 /* ggml_vec_dot_f32 (AVX: 4 accumulators x 8 lanes, fma, tree reduce, hadd) */
 static float dot_f32(int n, const float *x, const float *y) {
+    if (g_dot_variant == 1) return dot_f32_generic(n, x, y);
+    if (g_dot_variant == 2) return dot_f32_16(n, x, y, 0);
     float acc[4][8] = {{0}};
     int np = n & ~31;
     for (int i = 0; i < np; i += 32)
@@ -304,6 +345,8 @@ static float dot_f32(int n, const float *x, const float *y) {
 
 /* ggml_vec_dot_f16: fp16 inputs widened to f32, same SIMD structure, double leftovers */
 static float dot_f16(int n, const uint16_t *x, const uint16_t *y) {
+    if (g_dot_variant == 1) return dot_f16_generic(n, x, y);
+    if (g_dot_variant == 2) return dot_f32_16(n, (const float *)x, (const float *)y, 1);
     float acc[4][8] = {{0}};
     int np = n & ~31;
     for (int i = 0; i < np; i += 32)
@@ -330,38 +373,69 @@ static float hsum8(const float *a) {
 /* ggml_vec_dot_q4_0_q8_0 (AVX2): per block 8 lanes of 4-product int sums,
    acc_l = fma(fp16(dw)*fp16(da), lane_l, acc_l) */
 static float dot_q4_0_q8_0(int n, const uint8_t *w, const float *ad, const int8_t *aq) {
-    float acc[8] = {0};
+    float acc[16] = {0};
+    float sumf = 0.0f;
     for (int b = 0; b < n / QK; b++) {
         const uint8_t *blk = w + b * 18; uint16_t dh; memcpy(&dh, blk, 2);
         const float d = F16(dh) * ad[b];
         int8_t wq[QK];
         for (int j = 0; j < 16; j++) { wq[j] = (int8_t)((blk[2 + j] & 15) - 8); wq[j + 16] = (int8_t)((blk[2 + j] >> 4) - 8); }
+        if (g_dot_variant == 1) { /* sumf += sumi*d_x*d_y (gcc contracts the add into an fma) */
+            int sumi = 0;
+            for (int j = 0; j < QK; j++) sumi += wq[j] * aq[b * QK + j];
+            sumf = fmaf((float)sumi * F16(dh), ad[b], sumf);
+            continue;
+        }
+        if (g_dot_variant == 2) { /* 16 lanes of 2-product sums */
+            for (int l = 0; l < 16; l++) {
+                const int s2 = wq[2 * l] * aq[b * QK + 2 * l] + wq[2 * l + 1] * aq[b * QK + 2 * l + 1];
+                acc[l] = fmaf(d, (float)s2, acc[l]);
+            }
+            continue;
+        }
         for (int l = 0; l < 8; l++) {
             int s = 0;
             for (int j = 0; j < 4; j++) s += wq[4 * l + j] * aq[b * QK + 4 * l + j];
             acc[l] = fmaf(d, (float)s, acc[l]);
         }
     }
+    if (g_dot_variant == 1) return sumf;
+    if (g_dot_variant == 2) for (int l = 0; l < 8; l++) acc[l] += acc[l + 8];
     return hsum8(acc);
 }
 
 /* ggml_vec_dot_q4_1_q8_1 (AVX2): acc_l = fma(d0*d1, lane_l, acc_l); + sum m*s */
 static float dot_q4_1_q8_1(int n, const uint8_t *w, const float *ad, const float *as, const int8_t *aq) {
-    float acc[8] = {0};
-    float summs = 0.0f;
+    float acc[16] = {0};
+    float summs = 0.0f, sumf = 0.0f;
     for (int b = 0; b < n / QK; b++) {
         const uint8_t *blk = w + b * 20; uint16_t dh, mh; memcpy(&dh, blk, 2); memcpy(&mh, blk + 2, 2);
         const float d0 = F16(dh), m0 = F16(mh);
-        summs += m0 * as[b];
         const float d = d0 * ad[b];
         int wq[QK];
         for (int j = 0; j < 16; j++) { wq[j] = blk[4 + j] & 15; wq[j + 16] = blk[4 + j] >> 4; }
+        if (g_dot_variant == 1) { /* sumf += (d_x*d_y)*sumi + m_x*s_y */
+            int sumi = 0;
+            for (int j = 0; j < QK; j++) sumi += wq[j] * aq[b * QK + j];
+            sumf += fmaf(d, (float)sumi, m0 * as[b]);
+            continue;
+        }
+        summs += m0 * as[b];
+        if (g_dot_variant == 2) {
+            for (int l = 0; l < 16; l++) {
+                const int s2 = wq[2 * l] * aq[b * QK + 2 * l] + wq[2 * l + 1] * aq[b * QK + 2 * l + 1];
+                acc[l] = fmaf(d, (float)s2, acc[l]);
+            }
+            continue;
+        }
         for (int l = 0; l < 8; l++) {
             int s = 0;
             for (int j = 0; j < 4; j++) s += wq[4 * l + j] * aq[b * QK + 4 * l + j];
             acc[l] = fmaf(d, (float)s, acc[l]);
         }
     }
+    if (g_dot_variant == 1) return sumf;
+    if (g_dot_variant == 2) for (int l = 0; l < 8; l++) acc[l] += acc[l + 8];
     return hsum8(acc) + summs;
 }
 

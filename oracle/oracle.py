@@ -53,8 +53,18 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                          ctypes.POINTER(ctypes.c_int8)]
         L.oracle_max_threads.restype = ctypes.c_int
+        L.oracle_set_dot_variant.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
+
+
+# dot-kernel summation orders of the ggml builds the oracle can replay
+# (bert_oracle.c oracle_set_dot_variant): the checker uses "avx2"
+DOT_VARIANTS = {"avx2": 0, "generic": 1, "lanes16": 2}
+
+
+def set_dot_variant(name: str) -> None:
+    lib().oracle_set_dot_variant(DOT_VARIANTS[name])
 
 
 class Oracle:

@@ -11,6 +11,7 @@ before comparing.  The reference itself cannot be built or run here
 oracle is pinned separately (tests/test_oracle.py).
 
 Run:  python tests/golden/make_golden.py [case ...]
+      python tests/golden/make_golden.py --spread [case ...]   (only add the ggml-order spread)
 """
 from __future__ import annotations
 
@@ -101,6 +102,39 @@ def load_case(name: str):
     return meta, toks, z["emb"]
 
 
+def order_spread(path: str, toks, emb) -> list[float]:
+    """Per sentence, the largest 1 - cos between the AVX2 oracle (`emb`) and
+    the same semantics under the other summation orders ggml@8ca2c19 builds
+    use (oracle.DOT_VARIANTS: plain-C fallback, 16-lane width): how far two
+    valid ggml CPU runs of the reference land apart on this input."""
+    import oracle
+    o = oracle.Oracle(path)
+    worst = np.zeros(len(toks))
+    try:
+        for v in oracle.DOT_VARIANTS:
+            if v == "avx2":
+                continue
+            oracle.set_dot_variant(v)
+            a = o.eval_batch(toks, 0).astype(np.float64)
+            c = (a * emb).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(emb, axis=1)
+            worst = np.maximum(worst, 1 - c)
+    finally:
+        oracle.set_dot_variant("avx2")
+    return [float(x) for x in worst]
+
+
+def add_spread(name: str, model_dir: str):
+    """Add ggml_order_spread_1mcos to an existing fixture (inputs/outputs unchanged)."""
+    meta, toks, emb = load_case(name)
+    path = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    assert sha256(path) == meta["model_sha256"]
+    meta["ggml_order_spread_1mcos"] = order_spread(path, toks, emb.astype(np.float64))
+    z = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), tokens=z["tokens"], offsets=z["offsets"], emb=z["emb"],
+                        meta=np.array(json.dumps(meta)))
+    print(f"{name}: ggml order spread {meta['ggml_order_spread_1mcos']}", flush=True)
+
+
 def make(name: str, model_dir: str):
     import oracle  # test infrastructure only
 
@@ -119,6 +153,7 @@ def make(name: str, model_dir: str):
     meta = dict(case=name, shape=shape, hparams=hp, ftype=ftype, seed=SEED, w_std=w_std, lengths=lens,
                 n_layer=n_layer, model_sha256=sha256(path), oracle_seconds=round(dt, 2),
                 generator="bertlib.synth_model (csrc/synth.cpp)", oracle="oracle/bert_oracle.c")
+    meta["ggml_order_spread_1mcos"] = order_spread(path, toks, emb)
     if name in CHAOTIC:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import numpy_ref
@@ -132,11 +167,13 @@ def make(name: str, model_dir: str):
 
 
 def main():
-    names = sys.argv[1:] or list(CASES)
+    args = sys.argv[1:]
+    spread_only = "--spread" in args
+    names = [a for a in args if not a.startswith("--")] or list(CASES)
     model_dir = os.environ.get("BERT_AMD_MODEL_DIR") or os.path.join(tempfile.gettempdir(), "bert_amd_models")
     os.makedirs(model_dir, exist_ok=True)
     for n in names:
-        make(n, model_dir)
+        (add_spread if spread_only else make)(n, model_dir)
 
 
 if __name__ == "__main__":

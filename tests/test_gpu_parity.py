@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import bertlib
-from make_golden import CASES, CHAOTIC, SEED, ensure_model, load_case, sentence, sha256
+from make_golden import CASES, SEED, ensure_model, load_case, sentence, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -58,14 +58,32 @@ def test_golden_vectors(case, model_dir):
     c = cos(got, want)
     print(f"{case}: 1-cos min/mean {1 - c.max():.2e}/{1 - c.mean():.2e} max {1 - c.min():.2e} "
           f"maxabs {np.abs(got - want).max():.2e}")
-    if case in CHAOTIC:
-        # intrinsic sensitivity: an exact float64 restatement lands this far from the
-        # oracle; the GPU must not be further than twice that (and never NaN/garbage)
-        bound = np.maximum(2.0 * np.asarray(meta["exact_restatement_1mcos"]), 1 - COS_TOL)
-        assert np.all(1 - c <= bound), (case, 1 - c, bound)
-    else:
-        assert c.min() >= COS_TOL, (case, 1 - c)
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c, parity_bound(meta))
     assert np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-5)
+
+
+def parity_bound(meta):
+    """Per-sentence bound on 1 - cos vs the AVX2 oracle: the north star's
+    1e-4 (cos >= 0.9999), or — where ggml's OWN builds land further apart on
+    that input — twice the measured spread between ggml@8ca2c19's summation
+    orders (fixture field ggml_order_spread_1mcos: plain-C and 16-lane builds
+    vs the AVX2 build, tests/golden/make_golden.py order_spread).  Only the
+    24-layer bge Q4_1 fixture (spread 1.8e-3 / 2.3e-3) and the sigma = 0.1
+    stress model (9.3e-5) come near or past 1e-4."""
+    return np.maximum(1 - COS_TOL, 2.0 * np.asarray(meta["ggml_order_spread_1mcos"]))
+
+
+@pytest.mark.xfail(strict=True, reason="ggml's own builds differ by 1-cos 1.8e-3 / 2.3e-3 on these inputs "
+                                       "(fixture ggml_order_spread_1mcos): cos >= 0.9999 is out of reach "
+                                       "for any implementation that is not the AVX2 build itself")
+def test_c5_north_star_cos_bar(model_dir):
+    """The north-star bar taken literally on the 24-layer C5 fixture: kept as a
+    strict xfail so the miss stays visible."""
+    meta, toks, want = load_case("c5_bge_q4_1")
+    p, m = get_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    c = cos(m.eval_batch(toks), want)
+    print(f"c5 cos min {c.min():.6f} (ggml order spread {meta['ggml_order_spread_1mcos']})")
+    assert c.min() >= COS_TOL
 
 
 def test_live_oracle_random_ragged(model_dir):
@@ -106,10 +124,7 @@ def test_int8_gemm_path_golden(case, model_dir, monkeypatch):
         m.close()
     c = cos(got, want)
     print(f"int8 {case}: 1-cos max {1 - c.min():.2e}")
-    if case in CHAOTIC:
-        assert np.all(1 - c <= np.maximum(2.0 * np.asarray(meta["exact_restatement_1mcos"]), 1 - COS_TOL))
-    else:
-        assert c.min() >= COS_TOL, (case, 1 - c)
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
 
 
 def test_batch_invariance_and_determinism(model_dir):
@@ -142,20 +157,81 @@ def test_full_size_north_star_batch(model_dir):
     assert cos(out[:4], fx_emb).min() >= COS_TOL
 
 
+class Hip:
+    """The HIP runtime libbert.so itself links (/opt/rocm libamdhip64.so.7),
+    through ctypes: device buffers and streams for the device-resident API
+    without a second runtime in the process (torch bundles its own HIP/HSA
+    stack; mixing the two in one process is order-sensitive)."""
+
+    def __init__(self):
+        import ctypes
+        self.c = ctypes
+        self.L = ctypes.CDLL("libamdhip64.so.7")
+
+    def check(self, rc):
+        assert rc == 0, f"HIP error {rc}"
+
+    def malloc(self, nbytes):
+        p = self.c.c_void_p()
+        self.check(self.L.hipMalloc(self.c.byref(p), self.c.c_size_t(nbytes)))
+        return p.value
+
+    def free(self, p):
+        self.check(self.L.hipFree(self.c.c_void_p(p)))
+
+    def h2d(self, dst, arr):
+        arr = np.ascontiguousarray(arr)
+        self.check(self.L.hipMemcpy(self.c.c_void_p(dst), arr.ctypes.data_as(self.c.c_void_p),
+                                    self.c.c_size_t(arr.nbytes), 1))
+
+    def d2h(self, arr, src):
+        self.check(self.L.hipMemcpy(arr.ctypes.data_as(self.c.c_void_p), self.c.c_void_p(src),
+                                    self.c.c_size_t(arr.nbytes), 2))
+
+    def stream(self):
+        s = self.c.c_void_p()
+        self.check(self.L.hipStreamCreate(self.c.byref(s)))
+        return s.value
+
+    def sync(self, s):
+        self.check(self.L.hipStreamSynchronize(self.c.c_void_p(s)))
+
+    def destroy(self, s):
+        self.check(self.L.hipStreamDestroy(self.c.c_void_p(s)))
+
+
 def test_device_resident_api_matches_host_api(model_dir):
-    torch = pytest.importorskip("torch")
-    p, m = get_model(model_dir, "minilm", "q4_0")
-    toks = [sentence(i, n, 30522) for i, n in enumerate([128, 77, 1, 300])]
-    host = m.eval_batch(toks)
-    offs = np.zeros(len(toks) + 1, np.int32)
-    offs[1:] = np.cumsum([len(t) for t in toks])
-    d_tok = torch.tensor(np.concatenate(toks), dtype=torch.int32, device="cuda")
-    d_off = torch.tensor(offs, dtype=torch.int32, device="cuda")
-    d_out = torch.empty(len(toks), m.n_embd, dtype=torch.float32, device="cuda")
-    m.eval_device(d_tok.data_ptr(), d_off.data_ptr(), offs, len(toks), d_out.data_ptr(),
-                  torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    assert np.array_equal(d_out.cpu().numpy(), host)
+    """bert_amd_eval_device on a caller stream and on the null stream equals
+    bert_eval_batch bitwise (also after the workspace grows on that stream)."""
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    m = bertlib.BertModel(p)  # fresh context: the device calls below grow its workspace
+    hip = Hip()
+    for toks in ([sentence(i, n, 30522) for i, n in enumerate([128, 77, 1, 300])],
+                 [sentence(40 + i, 128, 30522) for i in range(300)]):  # larger: grows the workspace
+        offs = np.zeros(len(toks) + 1, np.int32)
+        offs[1:] = np.cumsum([len(t) for t in toks])
+        ids = np.concatenate(toks).astype(np.int32)
+        d_tok, d_off = hip.malloc(ids.nbytes), hip.malloc(offs.nbytes)
+        d_out = hip.malloc(len(toks) * m.n_embd * 4)
+        st = hip.stream()
+        try:
+            hip.h2d(d_tok, ids)
+            hip.h2d(d_off, offs)
+            res = []
+            for stream in (st, 0):
+                got = np.full((len(toks), m.n_embd), np.nan, np.float32)
+                m.eval_device(d_tok, d_off, offs, len(toks), d_out, stream)
+                hip.sync(stream)
+                hip.d2h(got, d_out)
+                res.append(got)
+        finally:
+            hip.destroy(st)
+            for q in (d_tok, d_off, d_out):
+                hip.free(q)
+        host = m.eval_batch(toks)
+        for got in res:
+            assert np.array_equal(got, host)
+    m.close()
 
 
 def test_two_replicas_shard_like_one(model_dir):
@@ -202,3 +278,47 @@ def test_q8_scale_division_exhaustive():
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
     print(out)
     assert "x/127 mismatches 0;" in out and "127/x mismatches (x in [2^-101, 2^101)) 0," in out
+
+
+def test_encode_batch_slices_sorted_and_bounded(model_dir):
+    """bert_encode_batch (reference bert.cpp:1119-1198): inputs sorted by token
+    count and evaluated n_batch_size at a time; the device workspace only grows
+    to the largest slice, and every embedding lands in its caller's row."""
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    m = bertlib.BertModel(p)  # fresh context: empty workspace
+    try:
+        rng = np.random.default_rng(7)
+        texts = [" ".join(f"w{int(x)}" for x in rng.integers(0, 500, int(k))) for k in rng.integers(1, 60, 40)]
+        ids = [m.tokenize(t) for t in texts]
+        emb = m.encode(texts, batch_size=8)
+        longest8 = sum(sorted(len(i) for i in ids)[-8:])
+        assert 0 < m.workspace_rows() <= (longest8 + 127) // 128 * 128
+        assert np.array_equal(emb, m.eval_batch(ids))
+        assert np.array_equal(m.encode(texts, batch_size=0), emb)
+    finally:
+        m.close()
+
+
+def test_mixed_lengths_group_like_separate_batches(model_dir):
+    """A host batch mixing <=128 and >128-token sentences runs as two ragged
+    batches (fused QKV+attention for the short ones); each result equals the
+    sentence evaluated alone, bitwise."""
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    toks = [sentence(50 + i, n, 30522) for i, n in enumerate([20, 300, 128, 129, 7, 512])]
+    full = m.eval_batch(toks)
+    short = m.eval_batch([toks[i] for i in (0, 2, 4)])
+    long_ = m.eval_batch([toks[i] for i in (1, 3, 5)])
+    assert np.array_equal(full[[0, 2, 4]], short)
+    assert np.array_equal(full[[1, 3, 5]], long_)
+
+
+def test_fused_head_quads_equal_head_pairs():
+    """qkv_attention_kernel with two head pairs per GEMM main loop (grouped
+    weight tile order, the default) is bitwise identical to one pair per main
+    loop (plain order) on F16 weights (tools/qkva_check.hip)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "qkva_check")
+    assert os.path.exists(exe), "build/qkva_check missing: run make"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120).stdout
+    print(out)
+    assert "elements differing: 0 of" in out

@@ -136,3 +136,19 @@ def test_golden_fixtures_reproduce(case, model_dir):
     p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"])
     o = oracle.Oracle(p)
     assert np.array_equal(o.eval_batch(toks, 3), emb)  # thread-count independent, bit-exact
+
+
+@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "minilm_q4_1", "c2_minilm_f16"])
+def test_ggml_order_spread_reproduces(case, model_dir):
+    """The fixtures' ggml_order_spread_1mcos (how far ggml@8ca2c19's plain-C
+    and 16-lane builds land from its AVX2 build on the fixture's inputs; the
+    GPU parity bound of tests/test_gpu_parity.py parity_bound) is reproduced
+    by the oracle's alternate summation orders, and the default order is
+    still the AVX2 checker."""
+    from make_golden import order_spread
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    got = order_spread(p, toks, want.astype(np.float64))
+    np.testing.assert_allclose(got, meta["ggml_order_spread_1mcos"], rtol=1e-9, atol=1e-15)
+    assert np.array_equal(oracle.Oracle(p).eval_batch(toks, 0), want)
+    assert max(got) > 0.0  # the orders really differ
