@@ -229,7 +229,8 @@ struct bert_ctx {
     int32_t cls_id = 101, sep_id = 102, pad_id = 0;
     WordPieceTokenizer tokenizer;
     std::vector<std::unique_ptr<Replica>> reps;
-    bool i8 = false;  // O / FFN projections on the int8-MFMA GEMMs (use_i8)
+    // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
+    bool i8_o = false, i8_up = false, i8_down = false;
     std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
 };
 
@@ -416,13 +417,17 @@ size_t act_scale_bytes(int wtype) { return wtype == W_Q4_0 ? 2 : wtype == W_Q4_1
 // Activation buffers carry GEMM_BM spare rows: qkv_attention_kernel reads the
 // 128-row tile starting at each sentence's first token (rows past M are
 // zero-filled and masked).
-bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, int64_t K) {
+// The zero fill is enqueued on `st`, the stream whose kernels use the buffer
+// (a plain hipMemset goes to the null stream, which does not order with the
+// library's non-blocking streams: the first batch on a fresh workspace could
+// race it).
+bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, int64_t K, hipStream_t st) {
     rows += GEMM_BM;
     if (!dmalloc(track, &a.q, (size_t)rows * K * act_elem_bytes(wtype))) return false;
-    HIP_OK(hipMemset(a.q, 0, (size_t)rows * K * act_elem_bytes(wtype)));
+    HIP_OK(hipMemsetAsync(a.q, 0, (size_t)rows * K * act_elem_bytes(wtype), st));
     if (act_scale_bytes(wtype)) {
         if (!dmalloc(track, &a.d, (size_t)rows * (K / 32) * act_scale_bytes(wtype))) return false;
-        HIP_OK(hipMemset(a.d, 0, (size_t)rows * (K / 32) * act_scale_bytes(wtype)));
+        HIP_OK(hipMemsetAsync(a.d, 0, (size_t)rows * (K / 32) * act_scale_bytes(wtype), st));
     }
     return true;
 }
@@ -450,8 +455,8 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, h
     if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
         !dmalloc(w.allocs, &w.qk_lo, (size_t)rows * 2 * E * 2) || !dmalloc(w.allocs, &w.vt_hi, (size_t)rows * E * 2) ||
         !dmalloc(w.allocs, &w.vt_lo, (size_t)rows * E * 2) ||
-        !alloc_act(w.allocs, w.Xa, wt, rows, E) || !alloc_act(w.allocs, w.Ca, wt, rows, E) ||
-        !alloc_act(w.allocs, w.Ua, wt, rows, I) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
+        !alloc_act(w.allocs, w.Xa, wt, rows, E, st) || !alloc_act(w.allocs, w.Ca, wt, rows, E, st) ||
+        !alloc_act(w.allocs, w.Ua, wt, rows, I, st) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
         !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4) ||
         !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4))
         return false;
@@ -512,19 +517,22 @@ void drain_profile(Replica &R) {
         }                                                                                 \
     } while (0)
 
-// Q4 models can run the O / FFN projections on the int8-MFMA GEMMs
-// (gemm_i8.hip: in-kernel scale application, 1 B/weight, one isum MFMA per
-// block).  Opt-in (env BERT_AMD_I8=1, read at load): on MI355X they measure
-// slower than the split-fp16 GEMMs today, so the default keeps
-// the split-fp16 path.
-bool use_i8(const bert_ctx *ctx) { return ctx->i8; }
-
-bool i8_wanted(const bert_ctx *ctx) {
+// Q4 models run selected projections on the int8-MFMA GEMMs (gemm_i8.hip:
+// 1 B/weight, exact isum per block on the int8 MFMA, d_w * d_a applied in
+// the kernel like ggml's vec_dot).  Default: the FFN-up GEMM only — there it
+// beats the split-fp16 GEMM in the pipeline; for the O and FFN-down
+// projections (LayerNorm epilogues) it does not.  Env
+// BERT_AMD_I8 (read at load): "0" none, "1" / "all" all three, "up" default.
+void i8_select(bert_ctx *ctx) {
     const char *e = std::getenv("BERT_AMD_I8");
+    const std::string v = e ? e : "up";
     const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
-    return e && *e && *e != '0' && (ctx->wtype == W_Q4_0 || ctx->wtype == W_Q4_1) &&
-           i8_gemm_supported(EPI_GELU_ACT, I, E) && i8_gemm_supported(E == 384 ? EPI_LN : EPI_RESID, E, I) &&
-           i8_gemm_supported(E == 384 ? EPI_LN : EPI_RESID, E, E);
+    const bool q4 = ctx->wtype == W_Q4_0 || ctx->wtype == W_Q4_1;
+    const int ln = E == 384 ? EPI_LN : EPI_RESID;
+    const bool all = v == "1" || v == "all";
+    ctx->i8_up = q4 && (all || v == "up") && i8_gemm_supported(EPI_GELU_ACT, I, E);
+    ctx->i8_o = q4 && all && i8_gemm_supported(ln, E, E);
+    ctx->i8_down = q4 && all && i8_gemm_supported(ln, E, I);
 }
 
 // One encoder layer over the row group [row0, row0 + rows) (sentences
@@ -588,8 +596,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
         o.ln_w = L.ln1_w;
         o.ln_b = L.ln1_b;
         o.eps = hp.eps;
-        const bool i8 = use_i8(ctx);
-        if (i8) {
+        if (ctx->i8_o) {
             o.Wi = L.o8;
             if (E == 384) {
                 LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt, EPI_LN, o, (int)rows, st));
@@ -614,7 +621,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
         u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
         u.gelu.n_pad = (int)tables().gelu_pair.size();  // the pair view (kernels.hip gelu_lookup)
         u.gelu.cap = tables().gelu_cap;
-        if (i8) {
+        if (ctx->i8_up) {
             u.Wi = L.up8;
             LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt, EPI_GELU_ACT, u, (int)rows, st));
         } else {
@@ -632,7 +639,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
         dn.ln_w = L.ln2_w;
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
-        if (i8) {
+        if (ctx->i8_down) {
             dn.Wi = L.down8;
             if (E == 384) {
                 LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt, EPI_LN, dn, (int)rows, st));
@@ -878,15 +885,12 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                     for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
         }
         if (!upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
-        if (use_i8(ctx)) {
-            if (!upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) || !upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) ||
-                !upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I))
-                return false;
-        } else if (!upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E)) ||
-                   !upload_packed(tr, dl.up, repack(wt, up_rows, E)) ||
-                   !upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))) {
+        // each projection in the one format its GEMM reads (int8 or split fp16)
+        if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E))) ||
+            !(ctx->i8_up ? upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) : upload_packed(tr, dl.up, repack(wt, up_rows, E))) ||
+            !(ctx->i8_down ? upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I)
+                           : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))))
             return false;
-        }
         if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
             !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||
             !upload(tr, &dl.ln1_w, l.ln1_w->data, E * 4) || !upload(tr, &dl.ln1_b, l.ln1_b->data, E * 4) ||
@@ -1056,7 +1060,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
                 tables().gelu_pair.size(), tables().exp_c.compact.size());
         return nullptr;
     }
-    ctx->i8 = i8_wanted(ctx.get());
+    i8_select(ctx.get());
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {
