@@ -57,3 +57,10 @@ $(BUILD)/i8_bench$(I8_SUFFIX): tools/i8_bench.hip $(SRC)/gemm_i8.hip $(SRC)/kern
 $(BUILD)/qkva_check: tools/qkva_check.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
+
+# host code (GGUF reader/writer, tokenizer, quantiser) under ASan + UBSan, CPU only (tests/test_sanitizers.py)
+SAN_SRCS := $(SRC)/gguf_io.cpp $(SRC)/tokenizer.cpp $(SRC)/quantize.cpp $(SRC)/quantize_model.cpp $(SRC)/synth.cpp tools/host_sanitize.cpp
+$(BUILD)/host_sanitize: $(SAN_SRCS) $(wildcard $(SRC)/*.h) $(SRC)/unicode_tables.inc
+	@mkdir -p $(BUILD)
+	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer \
+	    -Iinclude -I$(SRC) $(SAN_SRCS) -o $@ -lpthread

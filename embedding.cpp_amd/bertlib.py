@@ -34,7 +34,7 @@ ABI_SYMBOLS = [
 EXT_SYMBOLS = [
     "bert_amd_load", "bert_amd_n_devices", "bert_amd_hparams", "bert_amd_eval_device",
     "bert_amd_profile_enable", "bert_amd_profile_read", "bert_amd_synth_model", "bert_amd_tokenize_json",
-    "bert_amd_workspace_rows", "bert_amd_last_error",
+    "bert_amd_debug_embed", "bert_amd_workspace_rows", "bert_amd_last_error",
 ]
 
 # model shapes of BASELINE.json's configs
@@ -92,6 +92,8 @@ def lib() -> ctypes.CDLL:
     L.bert_amd_tokenize_json.restype = ctypes.c_int32
     L.bert_amd_tokenize_json.argtypes = [ctypes.c_char_p, ctypes.c_char_p, I_P, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+    L.bert_amd_debug_embed.restype = ctypes.c_int32
+    L.bert_amd_debug_embed.argtypes = [ctypes.c_void_p, I_P, I_P, ctypes.c_int32, F_P, ctypes.c_void_p, ctypes.c_void_p]
     L.bert_amd_workspace_rows.restype = ctypes.c_int64
     L.bert_amd_workspace_rows.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     L.bert_amd_last_error.restype = ctypes.c_char_p
@@ -206,6 +208,22 @@ class BertModel:
                                            ctypes.c_void_p(d_out_ptr), ctypes.c_void_p(stream or None))
         if rc != 0:
             raise RuntimeError(f"bert_amd_eval_device failed ({rc}): {last_error()}")
+
+    def debug_embed(self, token_lists):
+        """The embeddings + LayerNorm stage alone: (X f32 [M, E], q [M, E], d [M, E/32] or None)."""
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(t, np.int32) for t in token_lists]))
+        offs = np.zeros(len(token_lists) + 1, np.int32)
+        offs[1:] = np.cumsum([len(t) for t in token_lists])
+        M, E, wt = len(ids), self.n_embd, self.hparams[6]
+        X = np.zeros((M, E), np.float32)
+        q = np.zeros((M, E), {0: np.float32, 1: np.float16, 2: np.int8, 3: np.int8}[wt])
+        d = np.zeros((M, E // 32), np.float16 if wt == 2 else np.float32) if wt in (2, 3) else None
+        rc = self.lib.bert_amd_debug_embed(self.ctx, ids.ctypes.data_as(I_P), offs.ctypes.data_as(I_P), len(token_lists),
+                                           X.ctypes.data_as(F_P), q.ctypes.data_as(ctypes.c_void_p),
+                                           d.ctypes.data_as(ctypes.c_void_p) if d is not None else None)
+        if rc != 0:
+            raise RuntimeError(f"bert_amd_debug_embed failed ({rc}): {last_error()}")
+        return X, q, d
 
     def workspace_rows(self, slot: int = 0) -> int:
         return int(self.lib.bert_amd_workspace_rows(self.ctx, slot))

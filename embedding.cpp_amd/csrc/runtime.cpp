@@ -51,6 +51,14 @@ void set_err(const char *fmt, ...) {
     g_err = buf;
 }
 
+#define HIP_OK_RC(expr, rc)                                                           \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            set_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return rc;                                                                \
+        }                                                                             \
+    } while (0)
 #define HIP_OK(expr)                                                                  \
     do {                                                                              \
         hipError_t e_ = (expr);                                                       \
@@ -657,6 +665,31 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
     return true;
 }
 
+// embed_ln's arguments for a batch resident in the replica's workspace
+EmbedArgs embed_args(const bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, int n_seqs,
+                     int64_t M) {
+    const HParams &hp = ctx->hp;
+    EmbedArgs ea;
+    ea.tokens = d_tok;
+    ea.offsets = d_off;
+    ea.rowpos = R.ws.rowpos;
+    ea.n_seqs = n_seqs;
+    ea.M = (int)M;
+    ea.E = hp.n_embd;
+    ea.n_vocab = hp.n_vocab;
+    ea.n_pos = hp.n_max_tokens;
+    ea.word = R.word;
+    ea.pos = R.pos;
+    ea.type = R.type;
+    ea.word_t = ea.pos_t = ea.type_t = W_F32;  // the replica holds f32 copies (table_f32)
+    ea.ln_w = R.ln_e_w;
+    ea.ln_b = R.ln_e_b;
+    ea.eps = hp.eps;
+    ea.X = R.ws.X;
+    ea.Xa = R.ws.Xa;
+    return ea;
+}
+
 // The fixed pipeline over a ragged batch already resident on the device.
 bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
                   int n_seqs, float *d_out, hipStream_t st) {
@@ -674,24 +707,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     static const bool force_unfused = std::getenv("BERT_AMD_UNFUSED") != nullptr;
     const bool fused_qkv_attn = !force_unfused && qkv_attention_supported(wt, E, H, max_len);
 
-    EmbedArgs ea;
-    ea.tokens = d_tok;
-    ea.offsets = d_off;
-    ea.rowpos = w.rowpos;
-    ea.n_seqs = n_seqs;
-    ea.M = (int)M;
-    ea.E = E;
-    ea.n_vocab = hp.n_vocab;
-    ea.n_pos = hp.n_max_tokens;
-    ea.word = R.word;
-    ea.pos = R.pos;
-    ea.type = R.type;
-    ea.word_t = ea.pos_t = ea.type_t = W_F32;  // the replica holds f32 copies (table_f32)
-    ea.ln_w = R.ln_e_w;
-    ea.ln_b = R.ln_e_b;
-    ea.eps = hp.eps;
-    ea.X = w.X;
-    ea.Xa = w.Xa;
+    const EmbedArgs ea = embed_args(ctx, R, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(wt, ea, (int)Mpad, st));
 
     // Row groups (opt-in, env BERT_AMD_SPLIT=1): with the fused QKV + attention
@@ -1467,6 +1483,49 @@ int32_t bert_amd_profile_read(bert_ctx *ctx, char *names_buf, int32_t names_len,
         i++;
     }
     return i;
+}
+
+int32_t bert_amd_debug_embed(bert_ctx *ctx, const int32_t *tokens, const int32_t *offsets, int32_t n_seqs,
+                             float *X_out, void *q_out, void *d_out) {
+    if (!ctx || !tokens || !offsets || n_seqs <= 0 || !X_out || !q_out) {
+        set_err("bert_amd_debug_embed: invalid arguments");
+        return -1;
+    }
+    const int64_t M = offsets[n_seqs];
+    for (int s = 0; s < n_seqs; s++)
+        if (offsets[s + 1] - offsets[s] <= 0 || offsets[s + 1] - offsets[s] > ctx->hp.n_max_tokens) {
+            set_err("bert_amd_debug_embed: bad sentence length");
+            return -2;
+        }
+    for (int64_t i = 0; i < M; i++)
+        if (tokens[i] < 0 || tokens[i] >= ctx->hp.n_vocab) {
+            set_err("bert_amd_debug_embed: token id out of range");
+            return -2;
+        }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    try {
+        Replica &R = *ctx->reps[0];
+        HIP_OK_RC(hipSetDevice(R.device), -3);
+        const hipStream_t st = R.stream;
+        const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
+        if (!ensure_workspace(ctx, R, Mpad, n_seqs, st)) return -3;
+        Workspace &w = R.ws;
+        HIP_OK_RC(hipMemcpyAsync(w.tok, tokens, (size_t)M * 4, hipMemcpyHostToDevice, st), -3);
+        HIP_OK_RC(hipMemcpyAsync(w.off, offsets, (size_t)(n_seqs + 1) * 4, hipMemcpyHostToDevice, st), -3);
+        const EmbedArgs ea = embed_args(ctx, R, w.tok, w.off, n_seqs, M);
+        HIP_OK_RC(launch_embed(ctx->wtype, ea, (int)Mpad, st), -4);
+        const int64_t E = ctx->hp.n_embd;
+        HIP_OK_RC(hipMemcpyAsync(X_out, w.X, (size_t)(M * E) * 4, hipMemcpyDeviceToHost, st), -3);
+        HIP_OK_RC(hipMemcpyAsync(q_out, w.Xa.q, (size_t)(M * E) * act_elem_bytes(ctx->wtype), hipMemcpyDeviceToHost, st), -3);
+        if (d_out && act_scale_bytes(ctx->wtype))
+            HIP_OK_RC(hipMemcpyAsync(d_out, w.Xa.d, (size_t)(M * (E / 32)) * act_scale_bytes(ctx->wtype),
+                                     hipMemcpyDeviceToHost, st), -3);
+        HIP_OK_RC(hipStreamSynchronize(st), -3);
+    } catch (const std::exception &e) {
+        set_err("%s", e.what());
+        return -5;
+    }
+    return 0;
 }
 
 int64_t bert_amd_workspace_rows(bert_ctx *ctx, int32_t slot) {

@@ -72,6 +72,16 @@ BERT_API int32_t bert_amd_tokenize_json(const char *tokenizer_json, const char *
                                         int32_t n_max_tokens, int32_t frame, int32_t cls_id, int32_t sep_id,
                                         int32_t pad_id);
 
+/* Test hook: the embeddings + LayerNorm stage alone (reference
+   bert.cpp:865-898) on a host batch (packed ids + offsets[n_seqs+1]), on
+   replica 0.  Copies back X (f32 [M][n_embd], the LayerNorm output) and the
+   first GEMM's activation format of it: q [M][n_embd] (int8 for Q4 models,
+   fp16 / f32 for F16 / F32) and d [M][n_embd/32] (fp16 for Q4_0, f32 for
+   Q4_1; may be NULL).  Lets tests pin the integer stage bit-exactly against
+   the oracle's quantiser. */
+BERT_API int32_t bert_amd_debug_embed(struct bert_ctx *ctx, const int32_t *tokens, const int32_t *offsets,
+                                      int32_t n_seqs, float *X_out, void *q_out, void *d_out);
+
 /* Rows (tokens, padded to the 128-row tile) the device workspace of replica
    `slot` currently holds; -1 on a bad argument.  Lets callers and tests see
    that bert_encode_batch's n_batch_size bounds the working set. */

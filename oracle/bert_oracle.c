@@ -506,17 +506,11 @@ static void layer_norm(float *x, int N, int E, const gtensor *w, const gtensor *
 }
 
 /* one sentence: reference bert_build (bert.cpp:845-1012) + compute */
-int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
-    omodel *m = (omodel *)vm;
-    if (!m || N <= 0 || N > m->n_max) return -1;
-    const int E = m->n_embd, I = m->n_inter, H = m->n_head, D = E / H;
-    for (int i = 0; i < N; i++) if (tokens[i] < 0 || tokens[i] >= m->word->ne[1]) return -2;
-    float *x = (float *)malloc((size_t)N * E * 4), *tmp = (float *)malloc((size_t)N * E * 4);
-    float *qkv = (float *)malloc((size_t)3 * N * E * 4), *ctx = (float *)malloc((size_t)N * E * 4);
-    float *u = (float *)malloc((size_t)N * I * 4), *x1 = (float *)malloc((size_t)N * E * 4);
+/* embeddings: pos + (type[0] + word[id]) (bert.cpp:880-887), then the
+   embedding LayerNorm (bert.cpp:889-898), into x[N][E] */
+static void embed_ln(const omodel *m, const int32_t *tokens, int N, float *x) {
+    const int E = m->n_embd;
     float *typ = (float *)malloc((size_t)E * 4);
-
-    /* embeddings: pos + (type[0] + word[id])  (bert.cpp:880-887) */
     dequant_row(m->type->type, m->type->data, typ, E);
 #pragma omp parallel for schedule(static)
     for (int t = 0; t < N; t++) {
@@ -527,6 +521,27 @@ int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
         free(w); free(p);
     }
     layer_norm(x, N, E, m->ln_e_w, m->ln_e_b, m->eps);
+    free(typ);
+}
+
+/* the embedding stage alone (tests pin the GPU's embed_ln against it) */
+int oracle_embed_ln(void *vm, const int32_t *tokens, int N, float *x_out) {
+    omodel *m = (omodel *)vm;
+    if (!m || N <= 0 || N > m->n_max) return -1;
+    for (int i = 0; i < N; i++) if (tokens[i] < 0 || tokens[i] >= m->word->ne[1]) return -2;
+    embed_ln(m, tokens, N, x_out);
+    return 0;
+}
+
+int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
+    omodel *m = (omodel *)vm;
+    if (!m || N <= 0 || N > m->n_max) return -1;
+    const int E = m->n_embd, I = m->n_inter, H = m->n_head, D = E / H;
+    for (int i = 0; i < N; i++) if (tokens[i] < 0 || tokens[i] >= m->word->ne[1]) return -2;
+    float *x = (float *)malloc((size_t)N * E * 4), *tmp = (float *)malloc((size_t)N * E * 4);
+    float *qkv = (float *)malloc((size_t)3 * N * E * 4), *ctx = (float *)malloc((size_t)N * E * 4);
+    float *u = (float *)malloc((size_t)N * I * 4), *x1 = (float *)malloc((size_t)N * E * 4);
+    embed_ln(m, tokens, N, x);
 
     const float kq_scale = 1.0f / sqrtf((float)D);
     for (int il = 0; il < m->n_layer; il++) {
@@ -599,7 +614,7 @@ int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
     const float r = 1.0f / len;
     for (int e = 0; e < E; e++) out[e] = out[e] * r;
     free(col); free(inv);
-    free(x); free(tmp); free(qkv); free(ctx); free(u); free(x1); free(typ);
+    free(x); free(tmp); free(qkv); free(ctx); free(u); free(x1);
     return 0;
 }
 

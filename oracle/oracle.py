@@ -54,6 +54,9 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_int8)]
         L.oracle_max_threads.restype = ctypes.c_int
         L.oracle_set_dot_variant.argtypes = [ctypes.c_int]
+        L.oracle_embed_ln.restype = ctypes.c_int
+        L.oracle_embed_ln.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_float)]
         _lib = L
     return _lib
 
@@ -81,6 +84,16 @@ class Oracle:
         if getattr(self, "m", None):
             self.L.oracle_free(self.m)
             self.m = None
+
+    def embed_ln(self, tokens) -> np.ndarray:
+        """The embeddings + LayerNorm stage of one sentence (reference bert.cpp:865-898): [N, E] f32."""
+        t = np.ascontiguousarray(np.asarray(tokens, np.int32))
+        out = np.zeros((len(t), self.n_embd), np.float32)
+        rc = self.L.oracle_embed_ln(self.m, t.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(t),
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        if rc != 0:
+            raise RuntimeError(f"oracle_embed_ln failed ({rc})")
+        return out
 
     def eval_batch(self, token_lists, n_threads: int = 0) -> np.ndarray:
         lens = [len(t) for t in token_lists]

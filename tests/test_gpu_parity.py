@@ -347,3 +347,28 @@ def test_fresh_context_first_batch(model_dir):
             assert np.array_equal(first, m.eval_batch(toks))
         finally:
             m.close()
+
+
+@pytest.mark.parametrize("ftype", ["q4_0", "q4_1", "f16"])
+def test_embed_stage_bit_exact(ftype, model_dir):
+    """Per-stage integer parity (reference bert.cpp:865-898, then the Q8
+    conversion ggml applies before the first mul_mat): the embed_ln kernel's
+    LayerNorm output X is within 1 ulp of the oracle's, and its activation
+    codes are BIT-identical to the oracle quantiser (ggml quantize_row_q8_0 /
+    q8_1, AVX2) applied to the same X — q, and d (fp16 for Q8_0, f32 for
+    Q8_1); for F16 weights the fp16 conversion is bit-identical (RNE)."""
+    import oracle
+    p, m = get_model(model_dir, "minilm", ftype)
+    toks = [sentence(300 + i, n, 30522) for i, n in enumerate([17, 128, 1, 64])]
+    X, q, d = m.debug_embed(toks)
+    orc = oracle.Oracle(p)
+    ref = np.concatenate([orc.embed_ln(t) for t in toks])
+    ulp = np.abs(X.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+    print(f"{ftype}: X max ulp {ulp.max()}, exact {np.mean(ulp == 0):.4f}")
+    assert ulp.max() <= 1
+    if ftype == "f16":
+        assert np.array_equal(q.view(np.uint16), X.astype(np.float16).view(np.uint16))
+        return
+    dq, _, qq = oracle.quantize_q8(X, q8_1=(ftype == "q4_1"))
+    assert np.array_equal(q.ravel(), qq)
+    assert np.array_equal(d.astype(np.float32).ravel(), dq)
