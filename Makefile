@@ -64,3 +64,14 @@ $(BUILD)/host_sanitize: $(SAN_SRCS) $(wildcard $(SRC)/*.h) $(SRC)/unicode_tables
 	@mkdir -p $(BUILD)
 	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer \
 	    -Iinclude -I$(SRC) $(SAN_SRCS) -o $@ -lpthread
+
+# The reference's own consumer programs (examples/server.cpp, main.cpp), compiled unchanged
+# against include/ and linked with build/libbert.so — only where the reference checkout is
+# present (this container); the binaries travel to the GPU box with the tree
+# (tests/test_gpu_parity.py::test_reference_server_drop_in runs the server there).
+REF ?= /root/reference
+$(BUILD)/ref_%: $(REF)/examples/%.cpp $(BUILD)/libbert.so include/bert.h include/ggml.h
+	$(CXX) -std=c++17 -O2 -Iinclude $< -o $@ -L$(BUILD) -lbert -Wl,-rpath,'$$ORIGIN'
+
+ref_consumers: $(BUILD)/ref_server $(BUILD)/ref_main
+.PHONY: ref_consumers

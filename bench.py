@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--pmc-csv", default=os.environ.get("BENCH_PMC_CSV", ""))
+    ap.add_argument("--host-runs", type=int, default=10, help="timed bert_eval_batch runs (host buffers), 0: skip")
+    ap.add_argument("--ragged-steps", type=int, default=10, help="variable-length batch steps, 0: skip")
     args = ap.parse_args()
 
     import torch
@@ -225,6 +227,7 @@ def main():
     # per-kernel durations: HIP events recorded by the library around every launch,
     # on the launch stream, in a separate pass of profile-steps steps right after
     # the timed region (the timed region itself carries no events)
+    log(f"timed: {value:.1f} emb/s; per-kernel event pass")
     model.profile(True)
     for _ in range(args.profile_steps):
         step()
@@ -256,8 +259,23 @@ def main():
             ach = by / avg_s / 1e9
             roofline = dict(kernel=dominant, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                             frac=round(ach / PEAK_HBM_GBS, 4), bytes_per_launch=by)
-        traffic = pmc_traffic(args.pmc_csv, KERNEL_SYMBOL.get(dominant, dominant)) if args.pmc_csv else None
+        traffic, tsrc = None, None
+        if args.pmc_csv:
+            traffic = pmc_traffic(args.pmc_csv, KERNEL_SYMBOL.get(dominant, dominant))
+            tsrc = args.pmc_csv
+        else:
+            # corrected FETCH_SIZE x2 + WRITE_SIZE per launch measured by tools/profile_round.sh on
+            # this code for this workload (separate rocprofv3 --pmc passes; profiles/)
+            pf = os.path.join(REPO, "profiles", "pmc_traffic.json")
+            if os.path.exists(pf):
+                with open(pf) as f:
+                    pt = json.load(f)
+                wl = f"{args.shape} {args.ftype} batch={B} seq_len={N}"
+                if pt.get("workload") == wl and dominant in pt.get("bytes_per_launch", {}):
+                    traffic = pt["bytes_per_launch"][dominant]
+                    tsrc = f"profiles/pmc_traffic.json ({pt.get('source', '')})"
         roofline["traffic"] = traffic
+        roofline["traffic_source"] = tsrc
         roofline["algorithmic_bytes_per_launch"] = kernel_bytes(dominant, B, N, hp, args.ftype)
 
     # whole-path MFMA fraction: F(N) = L(8NE^2 + 4NEI + 4N^2E) per sentence
@@ -265,12 +283,61 @@ def main():
     f_sent = L * (8 * N * E * E + 4 * N * E * I + 4 * N * N * E)
     path_frac = f_sent * value / (world * PEAK_FP16_TFLOPS * 1e12)
 
+    # the reference ABI path (bert_eval_batch: host token lists in, host rows out,
+    # pinned H2D of the ids and D2H of the embeddings included), SURVEY §8(d):
+    # 3 warm-ups, median of 10 — reported beside `value`, never as it
+    host_api = None
+    if args.host_runs > 0:
+        log("host-API timing (bert_eval_batch)")
+        tl = toks  # [B, N] int32: bertlib builds the row pointer arrays by address arithmetic
+        for _ in range(3):
+            model.eval_batch(tl)
+        ts = []
+        for _ in range(args.host_runs):
+            h0 = time.perf_counter()
+            model.eval_batch(tl)
+            ts.append(time.perf_counter() - h0)
+        med = float(np.median(ts))
+        host_api = dict(value=round(B / med, 1), unit="embeddings/s", ms_median=round(med * 1e3, 3),
+                        ms_min=round(min(ts) * 1e3, 3), runs=args.host_runs,
+                        note="bert_eval_batch on host buffers, per GPU: ids H2D + embeddings D2H included")
+
+    # variable-length batch (server / MTEB-like sentences): lengths uniform in
+    # [8, 128], same sentence count, device-resident like the headline
+    ragged = None
+    if args.ragged_steps > 0:
+        log("variable-length batch timing")
+        rng = np.random.default_rng(SEED + rank)
+        lens = rng.integers(8, 129, B)
+        rtoks = [toks[i][:n].copy() for i, n in enumerate(lens)]
+        for t in rtoks:
+            t[-1] = 102
+        roffs = np.zeros(B + 1, np.int32)
+        roffs[1:] = np.cumsum(lens)
+        rd_tok = torch.from_numpy(np.concatenate(rtoks)).to(dev)
+        rd_off = torch.from_numpy(roffs).to(dev)
+        for _ in range(3):
+            model.eval_device(rd_tok.data_ptr(), rd_off.data_ptr(), roffs, B, d_out.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        r0 = time.perf_counter()
+        for _ in range(args.ragged_steps):
+            model.eval_device(rd_tok.data_ptr(), rd_off.data_ptr(), roffs, B, d_out.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        rdt = (time.perf_counter() - r0) / args.ragged_steps
+        ragged = dict(value=round(B / rdt, 1), unit="embeddings/s", ms_per_step=round(rdt * 1e3, 4),
+                      tokens_per_s=round(float(lens.sum()) / rdt, 1), lengths="uniform 8..128 (seeded)",
+                      mean_len=round(float(lens.mean()), 2), steps=args.ragged_steps)
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU checker + baseline only (never the measured path)
-        threads = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        # the CPUs this job may use: OMP_NUM_THREADS where the launcher sets the share (16 on the
+        # GPU box, whose os.cpu_count() is the whole host), else the affinity mask
+        avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or avail)
+        log(f"cpu baseline: {min(args.cpu_sample, B)} sentences on {threads} threads")
         S = min(args.cpu_sample, B)
         orc = oracle.Oracle(path)
         sample = [toks[i].tolist() for i in range(S)]
@@ -278,10 +345,17 @@ def main():
         c0 = time.perf_counter()
         ref = orc.eval_batch(sample, threads)
         c1 = time.perf_counter()
+        cpu_model = ""
+        try:
+            with open("/proc/cpuinfo") as f:
+                cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+        except OSError:
+            pass
         cpu = dict(value=round(S / (c1 - c0), 3), unit="embeddings/s", cores=threads, kind="port",
                    sample=f"first {S} of the {B} sentences (seq_len {N}), oracle/bert_oracle.c "
-                          f"(ggml-semantics C restatement, one sentence at a time, {threads} OpenMP threads, "
-                          f"-O3 -march=x86-64-v3)", seconds=round(c1 - c0, 2))
+                          f"(ggml-semantics C restatement, scalar C, not ggml's SIMD kernels; one sentence at a "
+                          f"time, {threads} OpenMP threads = the CPU share of this job, -O3 -march=x86-64-v3)",
+                   seconds=round(c1 - c0, 2), cpu_model=cpu_model, host_cpus=os.cpu_count())
         a = out[:S].astype(np.float64)
         c = (a * ref).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(ref, axis=1)
         parity = dict(cos_min=float(c.min()), cos_mean=float(c.mean()), n=S,
@@ -305,6 +379,8 @@ def main():
             "pipeline_mfma_frac": round(path_frac, 4),
             "kernels": kern,
             "cosine_vs_oracle": parity,
+            "host_api": host_api,
+            "ragged": ragged,
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)

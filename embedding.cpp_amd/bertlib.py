@@ -182,11 +182,21 @@ class BertModel:
         self.lib.bert_tokenize(self.ctx, text.encode("utf-8"), buf, ctypes.byref(n), n_max)
         return list(buf[: n.value])
 
-    def eval_batch(self, token_lists: Sequence[Sequence[int]]) -> np.ndarray:
-        """bert_eval_batch over host token lists -> [n, n_embd] float32."""
+    def eval_batch(self, token_lists: Union[Sequence[Sequence[int]], np.ndarray]) -> np.ndarray:
+        """bert_eval_batch over host token lists (or a 2-D int32 array of equal-length
+        sentences) -> [n, n_embd] float32."""
         n = len(token_lists)
-        arrs = [np.ascontiguousarray(np.asarray(t, dtype=np.int32)) for t in token_lists]
         emb = np.full((n, self.n_embd), np.nan, dtype=np.float32)
+        if isinstance(token_lists, np.ndarray) and token_lists.ndim == 2:
+            # fixed-length batch: the pointer arrays are address arithmetic (no per-row objects)
+            a = np.ascontiguousarray(token_lists, dtype=np.int32)
+            tptr = (a.ctypes.data + np.arange(n, dtype=np.uint64) * np.uint64(a.strides[0])).astype(np.uint64)
+            optr = (emb.ctypes.data + np.arange(n, dtype=np.uint64) * np.uint64(emb.strides[0])).astype(np.uint64)
+            ntok = np.full(n, a.shape[1], np.int32)
+            self.lib.bert_eval_batch(self.ctx, 1, n, ctypes.cast(tptr.ctypes.data, ctypes.POINTER(I_P)),
+                                     ntok.ctypes.data_as(I_P), ctypes.cast(optr.ctypes.data, ctypes.POINTER(F_P)))
+            return emb
+        arrs = [np.ascontiguousarray(np.asarray(t, dtype=np.int32)) for t in token_lists]
         tok_p = (I_P * n)(*[a.ctypes.data_as(I_P) for a in arrs])
         ntok = (ctypes.c_int32 * n)(*[len(a) for a in arrs])
         out_p = (F_P * n)(*[e.ctypes.data_as(F_P) for e in emb])

@@ -372,3 +372,62 @@ def test_embed_stage_bit_exact(ftype, model_dir):
     dq, _, qq = oracle.quantize_q8(X, q8_1=(ftype == "q4_1"))
     assert np.array_equal(q.ravel(), qq)
     assert np.array_equal(d.astype(np.float32).ravel(), dq)
+
+
+def test_reference_server_drop_in(model_dir):
+    """The reference's examples/server.cpp, compiled unchanged against
+    include/bert.h and linked with build/libbert.so (Makefile ref_consumers),
+    serves embeddings over its TCP protocol (reference server.cpp:26-118:
+    n_embd as an int on connect, then one text in -> n_embd floats out) equal
+    to bert_encode's, bitwise; the reference main.cpp prints the tokenisation."""
+    import socket
+    import subprocess
+    import time
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "build", "ref_server")
+    if not os.path.exists(exe):
+        pytest.skip("build/ref_server not built (needs the reference checkout at build time)")
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    with socket.socket() as s0:
+        s0.bind(("127.0.0.1", 0))
+        port = s0.getsockname()[1]
+    proc = subprocess.Popen([exe, "-m", p, "--port", str(port)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                            text=True)
+    try:
+        t0 = time.time()
+        lines = []
+        while time.time() - t0 < 60:
+            line = proc.stdout.readline()
+            lines.append(line)
+            if "Waiting for a client" in line or not line:
+                break
+        assert any("Server running" in l for l in lines), lines
+        texts = ["Should I get health insurance?", "Québec", "the quick brown fox " * 20]
+        with socket.create_connection(("127.0.0.1", port), timeout=60) as c:
+            n_embd = int(np.frombuffer(c.recv(4), np.int32)[0])
+            assert n_embd == m.n_embd
+            for t in texts:
+                c.sendall(t.encode())
+                buf = b""
+                while len(buf) < 4 * n_embd:
+                    chunk = c.recv(4 * n_embd - len(buf))
+                    assert chunk
+                    buf += chunk
+                got = np.frombuffer(buf, np.float32)
+                assert np.array_equal(got, m.encode(t)), t
+                time.sleep(0.05)  # one request per read() on the server side
+    finally:
+        proc.kill()
+        proc.wait(timeout=30)
+    main = os.path.join(repo, "build", "ref_main")
+    if os.path.exists(main):
+        r = subprocess.run([main, "-m", p, "-p", "Hello world"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "number of tokens in prompt" in r.stdout, r.stdout[-1000:] + r.stderr[-1000:]
+
+
+def test_eval_batch_2d_array_matches_lists(model_dir):
+    """bertlib's fixed-length fast path (row pointers by address arithmetic)
+    passes the same rows to bert_eval_batch as the list path."""
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    toks = np.array([sentence(900 + i, 64, 30522) for i in range(9)], np.int32)
+    assert np.array_equal(m.eval_batch(toks), m.eval_batch([list(t) for t in toks]))

@@ -1,0 +1,48 @@
+"""Per-launch HBM traffic of the bench's kernels from separate rocprofv3 --pmc
+FETCH_SIZE / WRITE_SIZE passes (tools/profile_round.sh), corrected as
+MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE counts half of the
+bytes of wide coalesced reads: doubled; both counters in KB), written as
+profiles/pmc_traffic.json for bench.py's roofline.traffic.
+python tools/pmc_traffic.py <fetch dir> <write dir> <workload> <out.json> [source note]"""
+import json
+import sys
+
+sys.path.insert(0, __file__.rsplit("/", 1)[0])
+from hbm_summary import load  # noqa: E402
+
+# bench.py kernel names -> fragments of the mangled kernel symbols
+NAMES = {
+    "qkv_attention": ["qkv_attention_kernel"],
+    "gemm_up_gelu": ["i8_up_gelu_kernel", "q4r_up_gelu_kernel", "gemm_kernelILi2ELi1", "gemm_kernel<2, 1,"],
+    "gemm_o_ln": ["gemm_kernelILi2ELi2", "gemm_kernel<2, 2,", "i8_ln384_kernel"],
+    "gemm_down_ln": ["gemm_kernelILi2ELi2", "gemm_kernel<2, 2,", "i8_ln384_kernel"],
+    "embed_ln": ["embed_ln_kernel"],
+    "pool_l2": ["pool_l2_kernel"],
+}
+
+
+def main():
+    fetch, write = load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE")
+    out = {"workload": sys.argv[3], "source": sys.argv[5] if len(sys.argv) > 5 else "", "bytes_per_launch": {},
+           "fetch_bytes": {}, "write_bytes": {},
+           "note": "FETCH_SIZE x2 + WRITE_SIZE, KB -> bytes, per dispatch; gemm_o_ln and gemm_down_ln share "
+                   "one kernel instantiation and are averaged together"}
+    for name, frags in NAMES.items():
+        fv, wv = [], []
+        for k in set(fetch) | set(write):
+            if any(f in k for f in frags):
+                fv += list(fetch.get(k, {}).values())
+                wv += list(write.get(k, {}).values())
+        if fv and wv:
+            fb = 2.0 * sum(fv) / len(fv) * 1024.0
+            wb = sum(wv) / len(wv) * 1024.0
+            out["fetch_bytes"][name] = round(fb)
+            out["write_bytes"][name] = round(wb)
+            out["bytes_per_launch"][name] = round(fb + wb)
+    with open(sys.argv[4], "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out["bytes_per_launch"]))
+
+
+if __name__ == "__main__":
+    main()
