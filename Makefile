@@ -47,11 +47,11 @@ $(BUILD)/div_check: tools/div_check.hip
 	@mkdir -p $(BUILD)
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -Wno-unused-value -Wno-unused-result $< -o $@
 
-# development timing harness for the int8-MFMA GEMMs (not shipped); I8_EXP=n compiles a timing ablation
-I8_EXP ?= 0
+# development timing harness for the int8-MFMA GEMMs (not shipped)
+
 $(BUILD)/i8_bench$(I8_SUFFIX): tools/i8_bench.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DI8_EXP=$(I8_EXP) $< -o $@
+	$(HIPCC) $(HIPFLAGS) $< -o $@
 
 # development check of the fused kernel's head-pair grouping, F16 (tools/qkva_check.hip)
 $(BUILD)/qkva_check: tools/qkva_check.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h

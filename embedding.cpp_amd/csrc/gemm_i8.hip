@@ -31,10 +31,6 @@ namespace bertamd {
 typedef int int4v __attribute__((ext_vector_type(4)));
 typedef int int16v __attribute__((ext_vector_type(16)));
 
-#ifndef I8_EXP
-#define I8_EXP 0  // development timing ablations (tools/i8_bench; wrong results), a bit mask: 1 no epilogue,
-                  // 2 no fold, 4 no weight loads, 8 no A chunk loads/stores, 16 no A fragment reads
-#endif
 
 // FFN-up kernel shape: waves per workgroup, f-tiles and t-tiles per wave
 // (tools/i8_bench sweeps them; 8 x 2 x 2 measured best)
@@ -146,17 +142,6 @@ template <int WT, int BM, int T, int BB>
 __device__ __forceinline__ void i8_aops(I8AOps<T> &o, const char *buf, int tt0) {
     using C = I8Chunk<BM, WT == W_Q4_1>;
     const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
-    if (I8_EXP & 16) {
-        if constexpr (BB == 0) {
-#pragma unroll
-            for (int t = 0; t < T; t++) {
-                o.xa[t] = *(const int4v *)(buf + (32 * (tt0 + t) + l32) * I8_LDQ + 16 * hh);
-                o.d16[t] = ((const uint16_t *)(buf + I8Chunk<BM, WT == W_Q4_1>::QB))[32 * (tt0 + t) + l32];
-                o.da[t] = 1.f;
-            }
-        }
-        return;
-    }
 #pragma unroll
     for (int t = 0; t < T; t++) {
         const int r = 32 * (tt0 + t) + l32;
@@ -191,14 +176,13 @@ struct I8Pipe {
     __device__ __forceinline__ void wload(const GemmArgs &g, int nkb, int ft0, int ft0n, int b) {
         const bool nx = b >= nkb;
         const int ft = nx ? ft0n : ft0, bb = nx ? b - nkb : b;
-        if (I8_EXP & 4) return;
 #pragma unroll
         for (int f = 0; f < F; f++) wf[S][f] = i8_wq(g.Wi, nkb, ft + f, bb);
     }
     // A chunk c of the tile at m0 and the weight scales of that chunk
     __device__ __forceinline__ void cload(const GemmArgs &g, int64_t m0, int ft0, int c) {
         const int lane = threadIdx.x & 63, nkb = g.K >> 5;
-        if (!(I8_EXP & 8)) i8_stage_load<WT, BM, NT>(st, g.A, g.K, m0, c * I8_KC);
+        i8_stage_load<WT, BM, NT>(st, g.A, g.K, m0, c * I8_KC);
 #pragma unroll
         for (int f = 0; f < F; f++) {
             if constexpr (WT == W_Q4_1) {
@@ -281,16 +265,12 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
         // results (left to itself the scheduler folds right behind the MFMA
         // that produces the operands and waits out its latency)
         __builtin_amdgcn_sched_barrier(0);
-#if I8_EXP & 2
-        asm volatile("" ::"v"(is[p & 1]), "v"(dd[p & 1]));
-#else
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             float v = __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], acc[p / T][p % T][i]);
             asm volatile("" : "+v"(v));  // keep the fold here: sunk past the MFMAs it would keep every tile live
             acc[p / T][p % T][i] = v;
         }
-#endif
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -346,7 +326,7 @@ __device__ __forceinline__ void i8_mainloop(const GemmArgs &g, int64_t m0, int f
         i8_block<WT, BM, F, T, 3, PIPE>(buf, tt0, pp.wf[3], ws, wd, wm, a1, a0, acc);
         pp.template wload<1>(g, nkb, ft0, ft0n, b0 + 5);
         if (more) {
-            if (!(I8_EXP & 8)) i8_stage_store<WT, BM, NT>(pp.st, smem + ((c + 1) & 1) * C::BYTES);
+            i8_stage_store<WT, BM, NT>(pp.st, smem + ((c + 1) & 1) * C::BYTES);
             wscale_use();
         }
         __syncthreads();
@@ -430,15 +410,6 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
         const int fc = ft0;
         m0 = m0n;
         ft0 = ft0n;
-        if (I8_EXP & 1) {
-            float z = 0.f;
-#pragma unroll
-            for (int f = 0; f < F; f++)
-#pragma unroll
-                for (int t = 0; t < T; t++) z += acc[f][t][0] + acc[f][t][15];
-            if (z == 1234.5f) g.X[tid] = z;
-            continue;
-        }
 #pragma unroll
         for (int f = 0; f < F; f++) {
             const int col = 32 * (fc + f) + 16 * hh;
@@ -614,10 +585,6 @@ __global__ __launch_bounds__(512) void i8_resid_kernel(GemmArgs g, int n_mtiles,
 // blocks).  The per-block fold is ggml's (isum exact on the int8 MFMA,
 // dd = d_w * d_a exact on an f16 MFMA: here d_w one-hot x the row's four d_a,
 // so the one-hot is built once per block and f-tile, not per t-tile).
-#ifndef Q4R_EXP
-#define Q4R_EXP 0  // development timing ablations of the q4r kernel (tools/i8_bench; wrong results), a bit mask:
-                   // 1 no epilogue, 2 no fold, 4 no weight loads, 8 no LDS-DMA, 16 no dd MFMA
-#endif
 namespace q4r {
 constexpr int BM = 128, T = 4, KC = 128, NBUF = 3;
 constexpr int AQ = BM * KC;     // int8 q of one chunk: 128 rows x 128 B (16 KiB)
@@ -670,7 +637,6 @@ struct Q4RStream {
 // pieces) into ring buffer `buf` (LDS byte address).
 template <int NWV>
 __device__ __forceinline__ void q4r_glds(const GemmArgs &g, const Q4RPos &P, uint32_t buf, int wv, int lane) {
-    if (Q4R_EXP & 8) return;
     const int K = g.K;
     for (int p = wv; p < q4r::APIECES; p += NWV) {
         const int row = 8 * p + (lane >> 3), sp = lane & 7, s = sp ^ q4r_swz(row);
@@ -685,7 +651,6 @@ __device__ __forceinline__ void q4r_glds(const GemmArgs &g, const Q4RPos &P, uin
 
 template <int NWV>
 __device__ __forceinline__ void q4r_wload(const GemmArgs &g, const Q4RPos &P, Q4RStream<NWV> &st, int lane) {
-    if (Q4R_EXP & 4) return;
     const int nkb = g.K >> 5;
 #pragma unroll
     for (int bb = 0; bb < 4; bb++) {
@@ -749,23 +714,16 @@ __device__ __forceinline__ void q4r_chunk(const char *abuf, const int4v (&w)[4],
         int16v is[2];
         float16v dd[2];
         is[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[bb], xa[0], cbias, 0, 0, 0);
-        dd[0] = (Q4R_EXP & 16) ? __builtin_bit_cast(float16v, cbias)
-                               : __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, oh),
-                                                                        __builtin_bit_cast(half8, dav[0]), zf, 0, 0, 0);
+        dd[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, oh), __builtin_bit_cast(half8, dav[0]),
+                                                       zf, 0, 0, 0);
 #pragma unroll
         for (int t = 0; t < 4; t++) {
             if (t + 1 < 4) {
                 is[(t + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[bb], xa[t + 1], cbias, 0, 0, 0);
-                dd[(t + 1) & 1] = (Q4R_EXP & 16) ? __builtin_bit_cast(float16v, cbias)
-                                                 : __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, oh),
+                dd[(t + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, oh),
                                                                          __builtin_bit_cast(half8, dav[t + 1]), zf, 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if (Q4R_EXP & 2) {
-                asm volatile("" ::"v"(is[t & 1]), "v"(dd[t & 1]));
-                __builtin_amdgcn_sched_barrier(0);
-                continue;
-            }
 #pragma unroll
             for (int i = 0; i < 16; i += 2) {
                 // (element copies first: clang's __builtin_bit_cast of an ext-vector
@@ -867,13 +825,6 @@ __global__ __launch_bounds__(NWV * 64) void q4r_up_gelu_kernel(GemmArgs g, int n
             q4r_wait_n<NWV>(st, P2.ok ? ng : 0);
             __builtin_amdgcn_s_barrier();
             slot = slot + 1 == q4r::NBUF ? 0 : slot + 1;
-        }
-        if (Q4R_EXP & 1) {
-            float z = 0.f;
-#pragma unroll
-            for (int t = 0; t < 4; t++) z += acc[t][0] + acc[t][15];
-            if (z == 1234.5f) g.X[tid] = z;
-            continue;
         }
         // y = gelu(b + W.x) -> Q8_0 (ggml: add(repeat(b), mul_mat), then gelu)
         const int col = 32 * Pt.ft + 16 * hh;

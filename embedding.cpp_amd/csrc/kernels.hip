@@ -57,13 +57,6 @@ __device__ __forceinline__ void ln_tasks(LnTask (&tk)[64 * NBLK / NT], int tid, 
 template <int NBLK, int NT>
 __device__ __forceinline__ void ln_xload(float4v (&xv)[64 * NBLK / NT][2], const LnTask (&tk)[64 * NBLK / NT],
                                          const float *X, int64_t row0) {
-#ifndef LN_EXP
-#define LN_EXP 0  // LN epilogue ablations (timing experiments only, wrong results): 1 no residual loads, 2 no stores, 3 no Q8 stores
-#endif
-#if LN_EXP == 1
-    for (int k = 0; k < 64 * NBLK / NT; k++) xv[k][0] = xv[k][1] = float4v{0.f, 0.f, 0.f, 0.f};
-    return;
-#endif
 #pragma unroll
     for (int k = 0; k < 64 * NBLK / NT; k++) {
         const float4v *xp = (const float4v *)(X + (row0 + tk[k].r) * (int64_t)(NBLK * 32) + tk[k].c);
@@ -141,18 +134,10 @@ __device__ __forceinline__ void ln_row_phase_q(float *stage, int ld, double *red
                 y[4 * h + j] = z + lb[j];
             }
         }
-#if LN_EXP == 2  // timing experiment only: no stores
-        float sum = 0.f;
-        for (int i = 0; i < 8; i++) sum += y[i];
-        if (sum == 1234.5678f) X[threadIdx.x] = sum;
-#else
         float4v *xo = (float4v *)(X + (row0 + tk[k].r) * (int64_t)ncols + tk[k].c);
         xo[0] = float4v{y[0], y[1], y[2], y[3]};
         xo[1] = float4v{y[4], y[5], y[6], y[7]};
-#if LN_EXP != 3  // 3: X stores only
         store_act_quarter<WT>(out, ncols, row0 + tk[k].r, tk[k].b, tk[k].qq, y);
-#endif
-#endif
     }
 }
 
@@ -555,10 +540,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
 
     const float4v zero4 = {0.f, 0.f, 0.f, 0.f};
     for (int kc = 0; kc < nkc; kc++) {
-#ifndef ML_EXP
-#define ML_EXP 0  // main-loop ablations (timing experiments only, wrong results): 2 no W reloads, 3 no A staging, 4 no barrier
-#endif
-        const bool more = kc + 1 < nkc && ML_EXP != 3;
+        const bool more = kc + 1 < nkc;
         if (more) {
 #pragma unroll
             for (int it = 0; it < IT; it++) {
@@ -569,26 +551,6 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
         const char *abuf = smem + (kc & 1) * A_BUF;
 #pragma unroll
         for (int kb = 0; kb < KB; kb++) {
-#ifdef GEMM_NOFOLD  // timing experiment only (wrong results): MFMA chain without the per-block fold
-            if constexpr (QP) {
-                half8 a[RT];
-#pragma unroll
-                for (int rt = 0; rt < RT; rt++)
-                    a[rt] = *(const half8 *)((const _Float16 *)abuf + (rt * 16 + c16) * LDA_H + kb * 32 + 8 * g);
-#pragma unroll
-                for (int nt = 0; nt < NTW; nt++)
-#pragma unroll
-                    for (int rt = 0; rt < RT; rt++) {
-                        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].hi, acc[rt][nt], 0, 0, 0);
-                        acc[rt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].lo, acc[rt][nt], 0, 0, 0);
-                    }
-                if (kc * KB + kb + 2 < nkb) {
-#pragma unroll
-                    for (int nt = 0; nt < NTW; nt++)
-                        wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
-                }
-            } else
-#endif
             if constexpr (QP) {
                 // Per (row tile, n-tile): blk = A.hi + A.lo  (two MFMAs: the exact
                 // d_w-scaled block dot product, f32-accumulated), then ONE fma
@@ -636,7 +598,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if (kc * KB + kb + 2 < nkb && ML_EXP != 2) {
+                if (kc * KB + kb + 2 < nkb) {
 #pragma unroll
                     for (int nt = 0; nt < NTW; nt++)
                         wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
@@ -684,7 +646,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 if (item < ITEMS) a_store<WT, BM>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
-        if (ML_EXP != 4) __syncthreads();
+        __syncthreads();
     }
 
 }
@@ -711,10 +673,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
     static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
-#ifndef GELU_LDS_TABLE
-#define GELU_LDS_TABLE 1
-#endif
-    constexpr bool GT_LDS = GELU_LDS_TABLE && EPI == EPI_GELU_ACT;
+    constexpr bool GT_LDS = EPI == EPI_GELU_ACT;
     __shared__ __attribute__((aligned(16))) uint16_t gtab[GT_LDS ? (GELU_T ? GELU_FLAT_LDS : HALF_TABLE_LDS) : 8];
 
     // XCD-aware tile order: linear block ids are dealt round-robin over the 8
@@ -733,19 +692,12 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
-#ifndef GELU_T_EXP
-#define GELU_T_EXP 0
-#endif
-#ifndef GELU_T_PRE
-#define GELU_T_PRE 0
-#endif
     if constexpr (GELU_T) {
         // ggml's GELU table, entries [0, 0x8000 + neg_n] (every positive pattern,
         // negatives up to the first of the constant run) -> LDS once per
         // workgroup; inputs below -|h(neg_n)| are clamped onto that entry.
         const int nflat8 = (0x8000 + args.gelu.neg_n + 1 + 7) / 8;
-        if (GELU_T_EXP != 3)
-            for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.full)[i];
+        for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.full)[i];
         const float xlo = h2f((uint16_t)(0x8000 | args.gelu.neg_n));
         int64_t m0;
         int n0;
@@ -757,12 +709,6 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
             gemm_mainloop<WT, NW, BM, NTW, true>(args, m0, (n0 + wv * WN) >> 4, smem, acc, pre);
             const int64_t mc = m0;
             const int nc = n0;
-#if GELU_T_PRE
-            if (t + (int)gridDim.x < nwg) {  // the next tile's first loads fly during this epilogue
-                tile_of(t + gridDim.x, m0, n0);
-                mainloop_preload(pre, args, m0, (n0 + wv * WN) >> 4);
-            }
-#endif
             // Transposed accumulators over W repacked in block-8 order
             // (gemm_gelu_blk8): lane (g, c16) holds acc[rt][2p + t][i] =
             // C[mc + 16 rt + c16][32 pb + 8 g + 4 t + i] (pb = the pair's
@@ -776,29 +722,16 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                     float y[8];
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-#if GELU_T_EXP == 1  // timing experiment only: skip the table
-                        y[i] = b0[i] + acc[rt][2 * p][i];
-                        y[4 + i] = b1[i] + acc[rt][2 * p + 1][i];
-#else
                         y[i] = h2f(gtab[f2h(fmaxf(b0[i] + acc[rt][2 * p][i], xlo))]);
                         y[4 + i] = h2f(gtab[f2h(fmaxf(b1[i] + acc[rt][2 * p + 1][i], xlo))]);
-#endif
                     }
-#if GELU_T_EXP == 2  // timing experiment only: no quantise / store
-                    float sum = 0.f;
-                    for (int i = 0; i < 8; i++) sum += y[i];
-                    if (sum == 1234.5678f) args.X[tid] = sum;
-#else
                     store_act_quarter_t<WT>(args.out_act, args.N, mc + rt * 16 + c16, col >> 5, g, y);
-#endif
                 }
             }
-#if !GELU_T_PRE
             if (t + (int)gridDim.x < nwg) {
                 tile_of(t + gridDim.x, m0, n0);
                 mainloop_preload(pre, args, m0, (n0 + wv * WN) >> 4);
             }
-#endif
         }
         return;
     }
@@ -815,10 +748,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     {
         MainloopPre<WT, NW, BM, NTW> pre;
         mainloop_preload(pre, args, m0, ntile0);
-#ifndef NONE_TRANS
-#define NONE_TRANS 0
-#endif
-        gemm_mainloop<WT, NW, BM, NTW, (NONE_TRANS && QP && EPI == EPI_NONE)>(args, m0, ntile0, smem, acc, pre);
+        gemm_mainloop<WT, NW, BM, NTW, false>(args, m0, ntile0, smem, acc, pre);
     }
 
     // ---- epilogue, in registers.  Lane (g, c16), pair p, row-tile rt, i:
@@ -942,11 +872,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                         const float4v v = *(const float4v *)(sp + 4 * h);
 #pragma unroll
                         for (int j = 0; j < 4; j++)
-#ifdef GELU_IDENTITY_EXPERIMENT  // timing experiment only: skip the table
-                            y[4 * h + j] = gb[k][h][j] + v[j];
-#else
                             y[4 * h + j] = h2f((uint16_t)gelu_lookup(tab, cap, f2h(gb[k][h][j] + v[j])));
-#endif
                     }
                     store_act_quarter<WT>(args.out_act, args.N, row0 + r, (n0 >> 5) + b, qq, y);
                 }
@@ -1248,19 +1174,6 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 // split hi/lo into the two heads' attention tiles in LDS, and the 8
 // (head, 32-query) attention tasks run as in attention_short_kernel.
 constexpr int QKVA_NW = 12, QKVA_D = 32;  // waves, head dim
-#ifdef QKVA_PROFILE  // development: per-phase shader-clock totals of thread 0 (tools/gemm_bench qkva)
-__device__ unsigned long long qkva_prof[4];
-#define QKVA_MARK(i)                                                   \
-    do {                                                               \
-        if (tid == 0) {                                                \
-            const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
-            atomicAdd(&qkva_prof[i], (unsigned long long)(t_ - t_last)); \
-            t_last = t_;                                               \
-        }                                                              \
-    } while (0)
-#else
-#define QKVA_MARK(i) do {} while (0)
-#endif
 
 template <int WT, int NTW>  // NTW: head pairs per main loop (qkv_attention_ntw)
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
@@ -1294,9 +1207,6 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     // row-major Q / K tiles), V waves the plain one (one dim x four adjacent
     // rows: 8-byte stores into V^T).
     const int hs_w = wv / 6, part_w = (wv % 6) / 2, d0 = 16 * (wv & 1);
-#ifdef QKVA_PROFILE
-    uint64_t t_last = __builtin_amdgcn_s_memtime();
-#endif
 
     for (int qd = 0; qd < a.H / (2 * NTW); qd++) {
         // heads 2 NTW qd ..: one main loop (one pass over the sentence's A panel)
@@ -1305,14 +1215,12 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
         // plays the one-pair role of the split below.
         const int64_t nt0 = (int64_t)qd * NTW * NW + NTW * wv;
         float4v acc[RT][NTW];
-        QKVA_MARK(0);
         MainloopPre<WT, NW, BM, NTW> pre;
         mainloop_preload(pre, g, beg, nt0);
         if (part_w == 2)  // ends with a barrier
             gemm_mainloop<WT, NW, BM, NTW, false>(g, beg, nt0, smem, acc, pre);
         else
             gemm_mainloop<WT, NW, BM, NTW, true>(g, beg, nt0, smem, acc, pre);
-        QKVA_MARK(1);
 #pragma unroll
         for (int half = 0; half < NTW; half++) {
             const int pr = NTW * qd + half;
@@ -1360,7 +1268,6 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                 }
             }
             __syncthreads();
-            QKVA_MARK(2);
 
             if (wv < 8) {  // attention task (head slot, 32 queries)
                 const int hs = wv >> 2, q0 = (wv & 3) * 32, head = 2 * pr + hs;
@@ -1424,7 +1331,6 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
             }
             __syncthreads();  // the next pair's tiles / the next quad's A chunks overwrite the attention tiles
         }
-        QKVA_MARK(3);
     }
 }
 

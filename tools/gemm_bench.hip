@@ -123,36 +123,6 @@ int main(int argc, char **argv) {
         run<W_Q4_0, EPI_LN, 384, 12, 128>("down LN   <384,12,128>", d, M, iters);
         run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
     }
-#ifdef QKVA_PROFILE
-    if (!strcmp(which, "qkva")) {  // fused QKV + attention, 1024 sentences of 128 tokens
-        const int S = M / 128;
-        std::vector<int32_t> offs(S + 1);
-        for (int i = 0; i <= S; i++) offs[i] = 128 * i;
-        int32_t *doffs;
-        CK(hipMalloc(&doffs, (S + 1) * 4));
-        CK(hipMemcpy(doffs, offs.data(), (S + 1) * 4, hipMemcpyHostToDevice));
-        AttnArgs a{};
-        a.offsets = doffs; a.E = E; a.H = 12; a.scale = 0.1767767f;
-        a.expt.compact = (const uint16_t *)dev_random(EXP_TABLE_LDS * 2, 7, 1);
-        a.expt.pos_n = 1; a.expt.neg_n = 19544; a.expt.n_pad = 19552;
-        a.ctx.q = oq; a.ctx.d = od;
-        GemmArgs qq = q;
-        hipEvent_t e0, e1;
-        CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-        for (int i = 0; i < 2; i++) CK(launch_qkv_attention(W_Q4_0, qq, a, S, 0));
-        unsigned long long z[4] = {0, 0, 0, 0};
-        CK(hipMemcpyToSymbol(HIP_SYMBOL(qkva_prof), z, sizeof z));
-        CK(hipEventRecord(e0, 0));
-        for (int i = 0; i < iters; i++) CK(launch_qkv_attention(W_Q4_0, qq, a, S, 0));
-        CK(hipEventRecord(e1, 0));
-        CK(hipEventSynchronize(e1));
-        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-        CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(qkva_prof), sizeof z));
-        const double tot = (double)z[0] + z[1] + z[2] + z[3];
-        printf("qkv_attention %.1f us/launch; phase shares: pre %.3f gemm %.3f split %.3f attn %.3f (cycles/WG %.0f)\n",
-               ms * 1000.0 / iters, z[0] / tot, z[1] / tot, z[2] / tot, z[3] / tot, tot / iters / S);
-    }
-#endif
     if (!strcmp(which, "upnone")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
     if (!strcmp(which, "gelu")) {
         run<W_Q4_0, EPI_GELU_ACT, 384, 12, 128>("up   GELU <384,12,128>", u, M, iters);

@@ -2,8 +2,6 @@
 // part of libbert.so): random Q8 activations and int8 weights at the MiniLM
 // shapes, each kernel timed with hipEvents over `iters` launches.
 //   build: make build/i8_bench      run: build/i8_bench [iters] [filter]
-// Timing ablations of the kernel itself are compiled in with -DI8_EXP=n
-// (gemm_i8.hip; wrong results, timing only).
 #include "../embedding.cpp_amd/csrc/gemm_i8.hip"
 
 #include <cstdio>
