@@ -302,13 +302,12 @@ def main():
                         ms_min=round(min(ts) * 1e3, 3), runs=args.host_runs,
                         note="bert_eval_batch on host buffers, per GPU: ids H2D + embeddings D2H included")
 
-    # variable-length batch (server / MTEB-like sentences): lengths uniform in
-    # [8, 128], same sentence count, device-resident like the headline
-    ragged = None
-    if args.ragged_steps > 0:
-        log("variable-length batch timing")
-        rng = np.random.default_rng(SEED + rank)
-        lens = rng.integers(8, 129, B)
+    # variable-length batches (server / MTEB-like sentences), same sentence
+    # count, device-resident like the headline: lengths uniform in [8, 128],
+    # and short ones in [8, 40] (several share a fused QKV+attention tile)
+    def ragged_line(lo, hi, salt):
+        rng = np.random.default_rng(SEED + rank + salt)
+        lens = rng.integers(lo, hi + 1, B)
         rtoks = [toks[i][:n].copy() for i, n in enumerate(lens)]
         for t in rtoks:
             t[-1] = 102
@@ -324,9 +323,15 @@ def main():
             model.eval_device(rd_tok.data_ptr(), rd_off.data_ptr(), roffs, B, d_out.data_ptr(), stream)
         torch.cuda.synchronize(dev)
         rdt = (time.perf_counter() - r0) / args.ragged_steps
-        ragged = dict(value=round(B / rdt, 1), unit="embeddings/s", ms_per_step=round(rdt * 1e3, 4),
-                      tokens_per_s=round(float(lens.sum()) / rdt, 1), lengths="uniform 8..128 (seeded)",
-                      mean_len=round(float(lens.mean()), 2), steps=args.ragged_steps)
+        return dict(value=round(B / rdt, 1), unit="embeddings/s", ms_per_step=round(rdt * 1e3, 4),
+                    tokens_per_s=round(float(lens.sum()) / rdt, 1), lengths=f"uniform {lo}..{hi} (seeded)",
+                    mean_len=round(float(lens.mean()), 2), steps=args.ragged_steps)
+
+    ragged = ragged_short = None
+    if args.ragged_steps > 0:
+        log("variable-length batch timing")
+        ragged = ragged_line(8, 128, 0)
+        ragged_short = ragged_line(8, 40, 1)
 
     cpu = None
     parity = None
@@ -381,6 +386,7 @@ def main():
             "cosine_vs_oracle": parity,
             "host_api": host_api,
             "ragged": ragged,
+            "ragged_short": ragged_short,
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)

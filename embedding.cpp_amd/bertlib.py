@@ -20,7 +20,8 @@ from typing import List, Sequence, Union
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(REPO, "build", "libbert.so")
+# BERT_AMD_LIB: another build of the library (development A/B runs only)
+LIB_PATH = os.environ.get("BERT_AMD_LIB") or os.path.join(REPO, "build", "libbert.so")
 
 F_P = ctypes.POINTER(ctypes.c_float)
 I_P = ctypes.POINTER(ctypes.c_int32)

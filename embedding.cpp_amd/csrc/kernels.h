@@ -133,6 +133,10 @@ struct AttnArgs {
     const uint16_t *vt_hi = nullptr, *vt_lo = nullptr;  // fp16 [E][ldv]: V^T
     int64_t ldv = 0;
     const int32_t *offsets = nullptr;
+    // qkv_attention_kernel only: tile t packs sentences tiles[2t] .. tiles[2t] +
+    // tiles[2t + 1] - 1 (their lengths rounded up to 32 sum to <= 128) into one
+    // workgroup; null: one sentence per workgroup
+    const int32_t *tiles = nullptr;
     int E = 0, H = 0;
     float scale = 0.f;                 // 1.0f / sqrtf(d_head)
     HalfTable expt;                    // ggml's fp16 exp table
@@ -151,7 +155,8 @@ hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs
 bool qkv_attention_supported(int wtype, int E, int H, int max_len);
 // head pairs per GEMM main loop of that kernel (its QKV copy's tile grouping, runtime.cpp)
 int qkv_attention_ntw(int wtype);
-hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s);
+// n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s);
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s);
 hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const float *b, float eps,
                      const ActPtr &out, hipStream_t s);

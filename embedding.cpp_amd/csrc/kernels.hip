@@ -1175,7 +1175,8 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 // (head, 32-query) attention tasks run as in attention_short_kernel.
 constexpr int QKVA_NW = 12, QKVA_D = 32;  // waves, head dim
 
-template <int WT, int NTW>  // NTW: head pairs per main loop (qkv_attention_ntw)
+// NTW: head pairs per main loop (qkv_attention_ntw); PK: sentence tiles (a.tiles)
+template <int WT, int NTW, bool PK>
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
     constexpr int D = QKVA_D, NW = QKVA_NW, BM = 128, RT = BM / 16;
@@ -1186,13 +1187,47 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     static_assert(NW * 16 == 2 * 3 * D, "one 16-feature n-tile per wave covers a head pair");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
-    const int s = blockIdx.x;
-    const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
-    if (n > NK || n <= 0) return;
+    // PK: a workgroup owns a tile of ns <= 4 consecutive sentences (AttnArgs.tiles:
+    // runtime.cpp packs them so that their lengths rounded up to 32 sum to
+    // <= 128); otherwise one sentence each (the single-sentence code is
+    // compiled without any of the packing logic).  The GEMM runs over the
+    // tile's n contiguous rows; in the attention tiles sentence j keeps its
+    // rows for Q and K but its V^T keys start at a 32-aligned slot vs_j, and
+    // its 32-query blocks get waves of their own, so every score, sum and P.V
+    // step of a sentence is the one it gets alone in a workgroup (results do
+    // not depend on the batch's other sentences, bit for bit).
+    __shared__ int qtab[PK ? 4 : 1][4];     // query block -> {first tile row of its sentence, length, first query, vs}
+    __shared__ uint8_t vslot[PK ? NK : 1];  // tile row -> V^T key slot
+    const int s0 = PK ? a.tiles[2 * blockIdx.x] : (int)blockIdx.x;
+    const int ns = PK ? a.tiles[2 * blockIdx.x + 1] : 1;
+    const int beg = a.offsets[s0], n = a.offsets[s0 + ns] - beg;
+    if (n > NK || n <= 0 || ns > 4) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int gq = lane >> 4, c16 = lane & 15, r = lane & 31, hh = lane >> 5;
     const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
     for (int i = tid; i < a.expt.n_pad / 8; i += NW * 64) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
+    if (PK && tid < NK) {  // read after the main loop's barriers
+        int b = 0, vs = 0, qb_b = 0, qb_len = 0, qb_q = 0, qb_vs = 0, slot = 0;
+        for (int j = 0; j < ns; j++) {
+            const int e = a.offsets[s0 + j + 1] - beg, len = e - b, span = (len + 31) & ~31;
+            if (tid >= b && tid < e) slot = vs + tid - b;
+            if (32 * tid >= vs && 32 * tid < vs + span) {
+                qb_b = b;
+                qb_len = len;
+                qb_q = 32 * tid - vs;
+                qb_vs = vs;
+            }
+            b = e;
+            vs += span;
+        }
+        vslot[PK ? tid : 0] = (uint8_t)slot;
+        if (tid < 4) {
+            qtab[PK ? tid : 0][0] = qb_b;
+            qtab[PK ? tid : 0][1] = qb_len;
+            qtab[PK ? tid : 0][2] = qb_q;
+            qtab[PK ? tid : 0][3] = qb_vs;
+        }
+    }
     auto slot = [&](int hs, int plane) -> _Float16 * {  // plane: 0 Qh 1 Ql 2 Kh 3 Kl 4 Vh 5 Vl
         char *base = smem + hs * SLOT;
         return (_Float16 *)(plane < 4 ? base + plane * NK * KST * 2 : base + 4 * NK * KST * 2 + (plane - 4) * D * VST * 2);
@@ -1235,6 +1270,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     asm volatile("" : "+v"(rl));
                     uint32_t off = (uint32_t)((char *)slot(hs_w, 4) - smem) + (uint32_t)((d0 + c16) * VST + 4 * gq) * 2;
                     asm volatile("" : "+v"(off));
+                    constexpr bool packed = PK;
 #pragma unroll
                     for (int rt = 0; rt < RT; rt++) {
                         half4v hv, lv;
@@ -1244,8 +1280,30 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                             hv[i] = (_Float16)y;
                             lv[i] = (_Float16)(y - (float)hv[i]);
                         }
+                        if constexpr (packed) {
+                            hv = half4v{};
+                            lv = half4v{};
+                        }
                         *(half4v *)(smem + off + rt * 32) = hv;
                         *(half4v *)(smem + off + D * VST * 2 + rt * 32) = lv;
+                    }
+                    if constexpr (packed) {
+                        // zeros first (key slots between sentences), then each row at its
+                        // sentence's slot: one wave's LDS writes land in program order
+                        const uint32_t voff = (uint32_t)((char *)slot(hs_w, 4) - smem) + (uint32_t)((d0 + c16) * VST) * 2;
+#pragma unroll
+                        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int row = 16 * rt + 4 * gq + i;
+                                if (row < n) {
+                                    const float y = b + acc[rt][half][i];
+                                    const _Float16 yh = (_Float16)y;
+                                    const uint32_t o2 = voff + 2u * vslot[row];
+                                    *(_Float16 *)(smem + o2) = yh;
+                                    *(_Float16 *)(smem + o2 + D * VST * 2) = (_Float16)(y - (float)yh);
+                                }
+                            }
                     }
                 } else {
                     const float4v b4 = *(const float4v *)(g.bias + fpair + 16 * wv + 4 * gq);
@@ -1269,30 +1327,45 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
             }
             __syncthreads();
 
-            if (wv < 8) {  // attention task (head slot, 32 queries)
-                const int hs = wv >> 2, q0 = (wv & 3) * 32, head = 2 * pr + hs;
-                if (q0 < n) {
+            if (wv < 8) {  // attention task (head slot, query block: 32 queries of one sentence)
+                const int hs = wv >> 2, qb = wv & 3, head = 2 * pr + hs;
+                int kb = 0, len = n, qrel = 32 * qb, vs = 0;
+                if constexpr (PK) {
+                    kb = qtab[qb][0];
+                    len = qtab[qb][1];
+                    qrel = qtab[qb][2];
+                    vs = qtab[qb][3];
+                }
+                if (PK ? len > 0 : qrel < n) {
                     const _Float16 *Qh = slot(hs, 0), *Ql = slot(hs, 1), *Kh = slot(hs, 2), *Kl = slot(hs, 3);
                     const _Float16 *Vh = slot(hs, 4), *Vl = slot(hs, 5);
+                    const int qrow = kb + qrel + r;  // tile row of this lane's query (rows past the
+                                                     // sentence read finite LDS data; never stored)
                     half8 qh[D / 16], ql[D / 16];
 #pragma unroll
                     for (int ks = 0; ks < D / 16; ks++) {
-                        qh[ks] = *(const half8 *)(Qh + (q0 + r) * KST + 16 * ks + 8 * hh);
-                        ql[ks] = *(const half8 *)(Ql + (q0 + r) * KST + 16 * ks + 8 * hh);
+                        qh[ks] = *(const half8 *)(Qh + qrow * KST + 16 * ks + 8 * hh);
+                        ql[ks] = *(const half8 *)(Ql + qrow * KST + 16 * ks + 8 * hh);
                     }
                     // two passes over the key tiles (the second recomputes the identical
                     // scores): only one 32-key score tile is live, which keeps this
                     // phase inside the 12-wave register budget next to the GEMM's.
                     // Pass 1 takes the max of the unscaled K.Q: x -> fl(x * scale) is
                     // monotonic for scale > 0, so fl(max * scale) is ggml's max of the
-                    // scaled scores.
-                    const int nkt = (n + 31) >> 5;
+                    // scaled scores.  Keys: the sentence's rows kb .. kb + len (K) and
+                    // slots vs .. vs + len (V^T); scores of keys >= len are masked.
+                    const int nkt = (len + 31) >> 5;
+                    int klim = lim;  // key 32 kt + (j & 3) + 8 (j >> 2) + 4 hh valid while < len
+                    if constexpr (PK) {
+                        klim = len - 4 * hh;
+                        asm volatile("" : "+v"(klim));
+                    }
                     auto scores = [&](int kt) {
-                        float16v S = attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql);
-                        if (32 * kt + 32 > n) {
+                        float16v S = attn_qk<D>(Kh, Kl, KST, kb + 32 * kt, r, hh, qh, ql);
+                        if (32 * kt + 32 > len) {
 #pragma unroll
                             for (int j = 0; j < 16; j++)
-                                if (32 * kt + (j & 3) + 8 * (j >> 2) >= lim) S[j] = -INFINITY;
+                                if (32 * kt + (j & 3) + 8 * (j >> 2) >= klim) S[j] = -INFINITY;
                         }
                         return S;
                     };
@@ -1323,10 +1396,10 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                             ph[j >> 3][j & 7] = __builtin_bit_cast(_Float16, pb);
                             sum += (uint32_t)(h2f(pb) * 16777216.0f);
                         }
-                        attn_pv_h<D>(o, Vh, Vl, VST, 32 * kt, r, hh, ph);
+                        attn_pv_h<D>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph);
                     }
                     sum += __shfl_xor(sum, 32);
-                    attn_store_ctx<WT, D>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + q0 + r, q0 + r < n, head, hh);
+                    attn_store_ctx<WT, D>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + qrow, qrel + r < len, head, hh);
                 }
             }
             __syncthreads();  // the next pair's tiles / the next quad's A chunks overwrite the attention tiles
@@ -1335,11 +1408,19 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 }
 
 template <int WT>
-static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
-    if (qkv_attention_ntw(WT) == 2)
-        hipLaunchKernelGGL((qkv_attention_kernel<WT, 2>), dim3(n_seqs), dim3(QKVA_NW * 64), 0, s, g, a);
-    else
-        hipLaunchKernelGGL((qkv_attention_kernel<WT, 1>), dim3(n_seqs), dim3(QKVA_NW * 64), 0, s, g, a);
+static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
+    const bool pk = a.tiles != nullptr;
+    if (qkv_attention_ntw(WT) == 2) {
+        if (pk)
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, 2, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+        else
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, 2, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+    } else {
+        if (pk)
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, 1, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+        else
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, 1, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+    }
     return hipGetLastError();
 }
 
@@ -1360,11 +1441,11 @@ bool qkv_attention_supported(int wtype, int E, int H, int max_len) {
            wtype != W_F32;
 }
 
-hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
     switch (wtype) {
-        case W_F16: return qkv_attn_t<W_F16>(g, a, n_seqs, s);
-        case W_Q4_0: return qkv_attn_t<W_Q4_0>(g, a, n_seqs, s);
-        case W_Q4_1: return qkv_attn_t<W_Q4_1>(g, a, n_seqs, s);
+        case W_F16: return qkv_attn_t<W_F16>(g, a, n_blocks, s);
+        case W_Q4_0: return qkv_attn_t<W_Q4_0>(g, a, n_blocks, s);
+        case W_Q4_1: return qkv_attn_t<W_Q4_1>(g, a, n_blocks, s);
     }
     return hipErrorInvalidValue;
 }

@@ -188,6 +188,8 @@ struct Workspace {
     uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16: kernels.h GemmArgs EPI_QKV
     ActPtr Xa, Ca, Ua;
     int32_t *tok = nullptr, *off = nullptr, *rowpos = nullptr;
+    int32_t *tiles = nullptr;  // qkv_attention_kernel's sentence tiles: [first, count] pairs
+    std::vector<int32_t> h_tiles;
     std::vector<void *> allocs;
     // pinned host staging for the host-pointer ABI
     int32_t *h_tok = nullptr, *h_off = nullptr;
@@ -457,7 +459,7 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, h
     w.X = w.out = nullptr;
     w.qk_hi = w.qk_lo = w.vt_hi = w.vt_lo = nullptr;
     w.Xa = w.Ca = w.Ua = ActPtr{};
-    w.tok = w.off = w.rowpos = nullptr;
+    w.tok = w.off = w.rowpos = w.tiles = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const int wt = ctx->wtype;
     if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
@@ -466,7 +468,7 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, h
         !alloc_act(w.allocs, w.Xa, wt, rows, E, st) || !alloc_act(w.allocs, w.Ca, wt, rows, E, st) ||
         !alloc_act(w.allocs, w.Ua, wt, rows, I, st) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
         !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4) ||
-        !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4))
+        !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4) || !dmalloc(w.allocs, &w.tiles, (size_t)seqs * 2 * 4))
         return false;
     // padding rows must hold finite values: zero everything once
     HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, st));
@@ -549,8 +551,8 @@ void i8_select(bert_ctx *ctx) {
 // the offsets, so they get the workspace bases (the unfused pair only runs
 // with one group, row0 == 0).
 bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
-               int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa, ActPtr Ca, ActPtr Ua, float *X,
-               hipStream_t st) {
+               const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
+               ActPtr Ca, ActPtr Ua, float *X, hipStream_t st) {
     const HParams &hp = ctx->hp;
     Workspace &w = R.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
@@ -587,7 +589,8 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
         if (fused_qkv_attn) {
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, nseq, st));
+            aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, st));
         } else {
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
@@ -740,6 +743,35 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
             HIP_OK(hipStreamWaitEvent(R.stream2, R.ev_fork, 0));
         }
     }
+    // Sentence tiles for the fused kernel: consecutive sentences packed greedily
+    // into one workgroup while their lengths rounded up to 32 sum to <= 128
+    // (kernels.hip qkv_attention_kernel: each keeps its own 32-query blocks and
+    // 32-aligned keys, so short sentences share the GEMM rows and the
+    // workgroup without changing a bit of their results).
+    int ntl[2] = {0, 0};
+    if (fused_qkv_attn) {
+        std::vector<int32_t> &ht = w.h_tiles;
+        ht.assign((size_t)2 * n_seqs, 0);
+        auto span = [&](int s) { return (h_off[s + 1] - h_off[s] + 31) & ~31; };
+        static const bool no_pack = std::getenv("BERT_AMD_NOPACK") != nullptr;  // A/B: one sentence a tile
+        for (int gi = 0; gi < ng; gi++) {
+            int32_t *t = ht.data() + 2 * G[gi].seq0;
+            for (int s = G[gi].seq0, e = G[gi].seq0 + G[gi].nseq; s < e;) {
+                int k = s + 1, used = span(s);
+                while (!no_pack && k < e && used + span(k) <= GEMM_BM) used += span(k++);
+                t[2 * ntl[gi]] = s - G[gi].seq0;
+                t[2 * ntl[gi] + 1] = k - s;
+                ntl[gi]++;
+                s = k;
+            }
+        }
+        // pageable source: the copy is staged before the call returns, so ht may be reused
+        HIP_OK(hipMemcpyAsync(w.tiles, ht.data(), (size_t)2 * n_seqs * 4, hipMemcpyHostToDevice, st));
+        if (ng == 2) {
+            HIP_OK(hipEventRecord(R.ev_fork, st));
+            HIP_OK(hipStreamWaitEvent(R.stream2, R.ev_fork, 0));
+        }
+    }
     const size_t eb = act_elem_bytes(wt), sb = act_scale_bytes(wt);
     auto act_rows = [&](ActPtr a, int64_t row0, int64_t K) {
         a.q = (char *)a.q + row0 * K * (int64_t)eb;
@@ -750,8 +782,8 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     for (int il = 0; il < hp.n_layer; il++)
         for (int gi = 0; gi < ng; gi++) {
             const Group &gr = G[gi];
-            if (!run_layer(ctx, R, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, max_len, fused_qkv_attn,
-                           ln_fused, act_rows(w.Xa, gr.row0, E), act_rows(w.Ca, gr.row0, E),
+            if (!run_layer(ctx, R, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, w.tiles + 2 * gr.seq0, ntl[gi],
+                           max_len, fused_qkv_attn, ln_fused, act_rows(w.Xa, gr.row0, E), act_rows(w.Ca, gr.row0, E),
                            act_rows(w.Ua, gr.row0, I), w.X + gr.row0 * E, gr.s))
                 return false;
         }

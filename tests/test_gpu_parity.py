@@ -322,6 +322,27 @@ def test_mixed_lengths_group_like_separate_batches(model_dir):
     assert np.array_equal(full[[1, 3, 5]], long_)
 
 
+@pytest.mark.parametrize("ftype", ["q4_0", "f16"])
+def test_packed_short_sentences_equal_alone(ftype, model_dir):
+    """Short sentences share a fused QKV+attention workgroup (runtime.cpp packs
+    consecutive sentences while their lengths rounded up to 32 sum to <= 128;
+    1 to 4 per tile).  Each keeps its own 32-query blocks and 32-aligned V^T
+    keys, so its embedding equals the sentence evaluated alone, bitwise, and
+    the batch stays within the north-star bar against the oracle."""
+    import oracle
+    p, m = get_model(model_dir, "minilm", ftype)
+    rng = np.random.default_rng(31)
+    lens = [1, 2, 3, 31, 32, 33, 5, 64, 64, 96, 32, 17, 9, 40, 100, 28] + rng.integers(1, 70, 48).tolist()
+    toks = [[101] + rng.integers(1000, 30522, max(n - 2, 0)).tolist() + [102] if n >= 2 else [101] for n in lens]
+    full = m.eval_batch(toks)
+    alone = np.stack([m.eval(t) for t in toks])
+    bad = [i for i in range(len(toks)) if not np.array_equal(full[i], alone[i])]
+    assert not bad, [(i, lens[i]) for i in bad]
+    sub = list(range(16))
+    c = cos(full[sub], oracle.Oracle(p).eval_batch([toks[i] for i in sub], 0))
+    assert c.min() >= COS_TOL, 1 - c
+
+
 def test_fused_head_quads_equal_head_pairs():
     """qkv_attention_kernel with two head pairs per GEMM main loop (grouped
     weight tile order, the default) is bitwise identical to one pair per main
