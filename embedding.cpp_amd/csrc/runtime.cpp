@@ -753,7 +753,9 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         std::vector<int32_t> &ht = w.h_tiles;
         ht.assign((size_t)2 * n_seqs, 0);
         auto span = [&](int s) { return (h_off[s + 1] - h_off[s] + 31) & ~31; };
-        static const bool no_pack = std::getenv("BERT_AMD_NOPACK") != nullptr;  // A/B: one sentence a tile
+        // env BERT_AMD_PACK (A/B and tests; read per batch): "0" never packs, "1" always
+        const char *pack_env = std::getenv("BERT_AMD_PACK");
+        const bool no_pack = pack_env && pack_env[0] == '0', force_pack = pack_env && pack_env[0] == '1';
         for (int gi = 0; gi < ng; gi++) {
             int32_t *t = ht.data() + 2 * G[gi].seq0;
             for (int s = G[gi].seq0, e = G[gi].seq0 + G[gi].nseq; s < e;) {
@@ -764,6 +766,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
                 ntl[gi]++;
                 s = k;
             }
+            if (!force_pack && !qkv_attention_pack_pays(G[gi].nseq, ntl[gi])) ntl[gi] = G[gi].nseq;  // plain kernel
         }
         // pageable source: the copy is staged before the call returns, so ht may be reused
         HIP_OK(hipMemcpyAsync(w.tiles, ht.data(), (size_t)2 * n_seqs * 4, hipMemcpyHostToDevice, st));

@@ -323,18 +323,24 @@ def test_mixed_lengths_group_like_separate_batches(model_dir):
 
 
 @pytest.mark.parametrize("ftype", ["q4_0", "f16"])
-def test_packed_short_sentences_equal_alone(ftype, model_dir):
+@pytest.mark.parametrize("pack", ["1", "auto"])
+def test_packed_short_sentences_equal_alone(ftype, pack, model_dir, monkeypatch):
     """Short sentences share a fused QKV+attention workgroup (runtime.cpp packs
     consecutive sentences while their lengths rounded up to 32 sum to <= 128;
-    1 to 4 per tile).  Each keeps its own 32-query blocks and 32-aligned V^T
-    keys, so its embedding equals the sentence evaluated alone, bitwise, and
-    the batch stays within the north-star bar against the oracle."""
+    1 to 4 per tile; "auto" packs when it saves workgroup rounds, which this
+    600-sentence batch does, "1" forces it).  Each keeps its own 32-query
+    blocks and 32-aligned V^T keys, so its embedding equals the sentence
+    evaluated alone, bitwise, and the batch stays within the north-star bar
+    against the oracle."""
     import oracle
     p, m = get_model(model_dir, "minilm", ftype)
     rng = np.random.default_rng(31)
-    lens = [1, 2, 3, 31, 32, 33, 5, 64, 64, 96, 32, 17, 9, 40, 100, 28] + rng.integers(1, 70, 48).tolist()
+    lens = [1, 2, 3, 31, 32, 33, 5, 64, 64, 96, 32, 17, 9, 40, 100, 28] + rng.integers(1, 70, 584).tolist()
     toks = [[101] + rng.integers(1000, 30522, max(n - 2, 0)).tolist() + [102] if n >= 2 else [101] for n in lens]
+    if pack == "1":
+        monkeypatch.setenv("BERT_AMD_PACK", "1")
     full = m.eval_batch(toks)
+    monkeypatch.setenv("BERT_AMD_PACK", "0")  # sentences alone: one per workgroup either way
     alone = np.stack([m.eval(t) for t in toks])
     bad = [i for i in range(len(toks)) if not np.array_equal(full[i], alone[i])]
     assert not bad, [(i, lens[i]) for i in bad]
