@@ -75,3 +75,8 @@ $(BUILD)/ref_%: $(REF)/examples/%.cpp $(BUILD)/libbert.so include/bert.h include
 
 ref_consumers: $(BUILD)/ref_server $(BUILD)/ref_main
 .PHONY: ref_consumers
+
+# development timing of the fused kernel's phases (tools/qkva_time.hip)
+$(BUILD)/qkva_time: tools/qkva_time.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $< -o $@

@@ -150,10 +150,10 @@ constexpr int ATT_QB = 64;    // queries per attention workgroup
 hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s);
 hipError_t launch_gemm(int wtype, int epi, int E_or_bn, const GemmArgs &a, int Mpad, hipStream_t s);
 hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs, int max_len, hipStream_t s);
-// QKV GEMM + attention in one kernel (sentences <= 128 tokens, head dim 32);
-// g: the QKV GemmArgs (head-major weights), a: the AttnArgs (its Q/K/V pointers unused)
 // whether packing n_seqs sentences into n_tiles workgroups is worth the packed variant
 bool qkv_attention_pack_pays(int n_seqs, int n_tiles);
+// QKV GEMM + attention in one kernel (sentences <= 128 tokens, head dim 32);
+// g: the QKV GemmArgs (head-major weights), a: the AttnArgs (its Q/K/V pointers unused)
 bool qkv_attention_supported(int wtype, int E, int H, int max_len);
 // head pairs per GEMM main loop of that kernel (its QKV copy's tile grouping, runtime.cpp)
 int qkv_attention_ntw(int wtype);

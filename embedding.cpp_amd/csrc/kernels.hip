@@ -1470,27 +1470,32 @@ hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a,
     return hipErrorInvalidValue;
 }
 
-// Attention for 128 < n <= 512: one workgroup per (128-query block, head,
-// sentence), wave w owning queries 32w..32w+31 of the block.  Keys stream
-// through LDS in 128-key chunks, twice: pass 1 finds every query's maximum
-// score; pass 2 recomputes the identical scores (same MFMA sequence) for
-// p = exp_tab[fp16(s - max)], the exact double sum and P.V.  So ggml's
+// Attention for 128 < n <= 512: one 8-wave workgroup per (256-query block,
+// head, sentence), wave w owning queries 32w..32w+31 of the block.  Keys
+// stream through LDS in 128-key chunks, twice: pass 1 finds every query's
+// maximum score; pass 2 recomputes the identical scores (same MFMA sequence)
+// for p = exp_tab[fp16(s - max)], the exact double sum and P.V.  So ggml's
 // soft_max (global max first) holds without materialising the n x n scores.
+// Eight waves share each staged chunk (two per SIMD, one workgroup per CU at
+// head dim 64: 110 KiB of LDS), so one wave's MFMAs cover the other's
+// softmax VALU and the chunk loads are amortised over 256 queries.
+constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, queries per workgroup
+
 template <int WT, int D>
-__global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
-    constexpr int NK = 128, KST = D + 8, VST = NK + 4;
+__global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnArgs a) {
+    constexpr int NK = 128, KST = D + 8, VST = NK + 4, NT = ATTN_LONG_NW * 64;
     __shared__ __attribute__((aligned(16))) _Float16 Kh[NK * KST], Kl[NK * KST], Vh[D * VST], Vl[D * VST];
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
     const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
-    if (n <= NK || qb * NK >= n) return;  // n <= 128: attention_short_kernel
+    if (n <= NK || qb * ATTN_LONG_QB >= n) return;  // n <= 128: attention_short_kernel
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
     const int E = a.E, E2 = 2 * E;
     const bool v_aligned = (beg & 7) == 0;
     const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
-    for (int i = tid; i < a.expt.n_pad / 8; i += 256) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
+    for (int i = tid; i < a.expt.n_pad / 8; i += NT) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
 
-    const int q0 = qb * NK + wv * 32;
+    const int q0 = qb * ATTN_LONG_QB + wv * 32;
     const bool active = q0 < n;  // wave-uniform
     half8 qh[D / 16], ql[D / 16];
     {
@@ -1505,14 +1510,15 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
     // The 2*nch stages (pass 1: K of chunk c; pass 2: K and V^T of chunk c)
     // are register-prefetched one stage ahead: KIT / VIT 16-byte pieces per
     // thread and plane.
-    constexpr int KIT = NK * (D / 8) / 256, VIT = D * (NK / 8) / 256;
+    constexpr int KIT = NK * (D / 8) / NT, VIT = D * (NK / 8) / NT;
+    static_assert(KIT * NT == NK * (D / 8) && VIT * NT == D * (NK / 8), "whole 16-byte pieces per thread");
     uint4 pkh[KIT], pkl[KIT];
     half8 pvh[VIT], pvl[VIT];
     auto fetch = [&](int c, bool with_v) {
         const int kbase = c * NK;
 #pragma unroll
         for (int i = 0; i < KIT; i++) {
-            const int idx = tid + 256 * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
+            const int idx = tid + NT * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
             pkh[i] = pkl[i] = uint4{0u, 0u, 0u, 0u};
             if (kbase + key < n) {
                 const int64_t off = (int64_t)(beg + kbase + key) * E2 + E + h * D + col;
@@ -1523,7 +1529,7 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
         if (!with_v) return;
 #pragma unroll
         for (int i = 0; i < VIT; i++) {
-            const int idx = tid + 256 * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+            const int idx = tid + NT * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
             const int64_t off = (int64_t)(h * D + d) * a.ldv + beg + kbase + k8;
             pvh[i] = pvl[i] = half8{};
             if (kbase + k8 + 8 <= n && v_aligned) {
@@ -1542,14 +1548,14 @@ __global__ __launch_bounds__(256) void attention_long_kernel(AttnArgs a) {
     auto commit = [&](bool with_v) {
 #pragma unroll
         for (int i = 0; i < KIT; i++) {
-            const int idx = tid + 256 * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
+            const int idx = tid + NT * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
             *(uint4 *)&Kh[key * KST + col] = pkh[i];
             *(uint4 *)&Kl[key * KST + col] = pkl[i];
         }
         if (!with_v) return;
 #pragma unroll
         for (int i = 0; i < VIT; i++) {
-            const int idx = tid + 256 * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
+            const int idx = tid + NT * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
             const half8 vh = pvh[i], vl = pvl[i];
             *(half4v *)&Vh[d * VST + k8] = half4v{vh[0], vh[1], vh[2], vh[3]};
             *(half4v *)&Vh[d * VST + k8 + 4] = half4v{vh[4], vh[5], vh[6], vh[7]};
@@ -1767,7 +1773,8 @@ static hipError_t attn_t(const AttnArgs &a, int n_seqs, int max_len, hipStream_t
     hipLaunchKernelGGL((attention_short_kernel<WT, D>), dim3(groups, n_seqs), dim3(256), 0, s, a, hpw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || max_len <= 128) return e;
-    hipLaunchKernelGGL((attention_long_kernel<WT, D>), dim3((max_len + 127) / 128, a.H, n_seqs), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attention_long_kernel<WT, D>), dim3((max_len + ATTN_LONG_QB - 1) / ATTN_LONG_QB, a.H, n_seqs),
+                       dim3(ATTN_LONG_NW * 64), 0, s, a);
     return hipGetLastError();
 }
 

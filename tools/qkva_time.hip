@@ -1,0 +1,108 @@
+// Development timing of the fused QKV + attention kernel's phases (not part of
+// libbert.so): qkv_attention_kernel<Q4_0, 2> at the C3 shape (1024 sentences x
+// 128 tokens, MiniLM), random operands, timed with hipEvents as shipped (K =
+// 384) and with the GEMM main loop emptied (K = 0: the attention phase, the
+// tile epilogues and the fixed per-workgroup costs only).
+//   build: make build/qkva_time      run: build/qkva_time [iters]
+#include "../embedding.cpp_amd/csrc/kernels.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace bertamd;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+static uint16_t h16(float f) { _Float16 h = (_Float16)f; uint16_t u; std::memcpy(&u, &h, 2); return u; }
+static float f16(uint16_t u) { _Float16 h; std::memcpy(&h, &u, 2); return (float)h; }
+
+static void *dev_random(size_t bytes, uint32_t seed, int kind) {
+    std::vector<uint8_t> h(bytes);
+    uint32_t x = seed * 2654435761u + 1;
+    for (size_t i = 0; i < bytes; i++) {
+        x = x * 1664525u + 1013904223u;
+        h[i] = (uint8_t)(x >> 24);
+    }
+    if (kind == 1) {  // fp16 in a modest range
+        uint16_t *p = (uint16_t *)h.data();
+        for (size_t i = 0; i < bytes / 2; i++) p[i] = (uint16_t)((p[i] & 0x83ff) | 0x2000);
+    }
+    void *d;
+    CK(hipMalloc(&d, bytes));
+    CK(hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice));
+    return d;
+}
+
+int main(int argc, char **argv) {
+    const int S = 1024, L = 128, E = 384, H = 12, D = 32, iters = argc > 1 ? atoi(argv[1]) : 20;
+    const int M = S * L, Mpad = M + 128;
+    std::vector<int32_t> offs(S + 1);
+    for (int s = 0; s <= S; s++) offs[s] = s * L;
+    int32_t *d_off;
+    CK(hipMalloc(&d_off, offs.size() * 4));
+    CK(hipMemcpy(d_off, offs.data(), offs.size() * 4, hipMemcpyHostToDevice));
+    std::vector<uint16_t> full(65536);
+    for (int i = 0; i < 65536; i++) full[i] = h16(expf(f16((uint16_t)i)));
+    const uint16_t nc = full[0xfbff];
+    int neg_n = 0x7c00;
+    while (neg_n > 0 && full[0x8000 | (neg_n - 1)] == nc) neg_n--;
+    std::vector<uint16_t> comp((size_t)(1 + neg_n + 1 + 7) / 8 * 8, 0);
+    comp[0] = full[0];
+    for (int m = 0; m < neg_n; m++) comp[1 + m] = full[0x8000 | m];
+    comp[1 + neg_n] = nc;
+    uint16_t *d_comp;
+    CK(hipMalloc(&d_comp, comp.size() * 2));
+    CK(hipMemcpy(d_comp, comp.data(), comp.size() * 2, hipMemcpyHostToDevice));
+
+    GemmArgs g{};
+    void *aq;
+    CK(hipMalloc(&aq, (size_t)Mpad * E));
+    CK(hipMemset(aq, 0x11, (size_t)Mpad * E));
+    g.A.q = aq;
+    g.A.d = dev_random((size_t)Mpad * (E / 32) * 4, 2, 1);
+    g.W.q = dev_random((size_t)3 * E * E * 4, 3, 1);
+    g.W.unscale = 1.0f / 16384;
+    g.bias = (const float *)dev_random((size_t)3 * E * 4, 4, 0);
+    CK(hipMemset((void *)g.bias, 0, (size_t)3 * E * 4));
+    g.K = E;
+    g.N = 3 * E;
+    g.head_dim = D;
+    AttnArgs a{};
+    a.offsets = d_off;
+    a.E = E;
+    a.H = H;
+    a.scale = 1.0f / sqrtf((float)D);
+    a.expt.compact = d_comp;
+    a.expt.pos_n = 1;
+    a.expt.neg_n = neg_n;
+    a.expt.n_pad = (int)comp.size();
+    void *cq, *cd;
+    CK(hipMalloc(&cq, (size_t)Mpad * E));
+    CK(hipMalloc(&cd, (size_t)Mpad * (E / 32) * 4));
+    a.ctx.q = cq;
+    a.ctx.d = cd;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int K : {E, 0}) {
+        g.K = K;
+        auto launch = [&] {
+            hipLaunchKernelGGL((qkv_attention_kernel<W_Q4_0, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
+        };
+        for (int i = 0; i < 3; i++) launch();
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; i++) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("qkv_attention q4_0 K=%d: %8.1f us\n", K, ms * 1000.0 / iters);
+        fflush(stdout);
+    }
+    return 0;
+}
