@@ -366,18 +366,23 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__r
 // lane owns two adjacent columns of 4 rows per pair: bias / GELU / Q8 / LN
 // epilogues run in registers and store 8-byte (f32) or 2-byte (int8) pieces
 // that coalesce into whole rows.
+// One thread's 16-element A piece in flight: 16 bytes (Q8 codes + the block's
+// d), 32 (fp16) or 64 (f32), as register vectors.  (Round 1 held them in a
+// 64-byte array of HIP uint4 structs: the struct copies global -> AReg -> LDS
+// became memcpys that kept the array in scratch, 176 B/lane in every F16 GEMM.)
+template <int WT>
 struct AReg {
-    uint4 r[4];
+    u32x4v r[WT == W_F32 ? 4 : WT == W_F16 ? 2 : 1];
     float d;
 };
 
 template <int WT>
-__device__ __forceinline__ void a_load(AReg &ar, const ActPtr &A, int K, int64_t m0, int k0, int item) {
+__device__ __forceinline__ void a_load(AReg<WT> &ar, const ActPtr &A, int K, int64_t m0, int k0, int item) {
     const int r = item >> 2, s = item & 3;
     const int64_t row = m0 + r;
     const int k = k0 + s * 16;
     if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
-        ar.r[0] = *(const uint4 *)((const int8_t *)A.q + row * K + k);
+        ar.r[0] = *(const u32x4v *)((const int8_t *)A.q + row * K + k);
         const int64_t bi = row * (K >> 5) + (k >> 5);
         if constexpr (WT == W_Q4_0) {
             ar.d = h2f(((const uint16_t *)A.d)[bi]);
@@ -385,11 +390,11 @@ __device__ __forceinline__ void a_load(AReg &ar, const ActPtr &A, int K, int64_t
             ar.d = ((const float *)A.d)[bi];
         }
     } else if constexpr (WT == W_F16) {
-        const uint4 *p = (const uint4 *)((const uint16_t *)A.q + row * K + k);
+        const u32x4v *p = (const u32x4v *)((const uint16_t *)A.q + row * K + k);
         ar.r[0] = p[0];
         ar.r[1] = p[1];
     } else {
-        const uint4 *p = (const uint4 *)((const float *)A.q + row * K + k);
+        const u32x4v *p = (const u32x4v *)((const float *)A.q + row * K + k);
         ar.r[0] = p[0];
         ar.r[1] = p[1];
         ar.r[2] = p[2];
@@ -408,20 +413,20 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t x, half2v &lo, half2v &hi) 
 }
 
 template <int WT, int BM, int LDA = LDA_H>
-__device__ __forceinline__ void a_store(const AReg &ar, char *buf, int item, float unscale) {
+__device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item, float unscale) {
     const int r = item >> 2, s = item & 3;
     constexpr int A_BYTES = (WT == W_F32) ? BM * LDA_F * 4 : BM * LDA * 2;
     if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
-        const uint32_t *w = (const uint32_t *)&ar.r[0];
+        const u32x4v w = ar.r[0];
         half8 h0, h1;
         half2v a, b;
-        i8x4_to_f16(w[0], a, b);
+        i8x4_to_f16(w.x, a, b);
         h0[0] = a[0]; h0[1] = a[1]; h0[2] = b[0]; h0[3] = b[1];
-        i8x4_to_f16(w[1], a, b);
+        i8x4_to_f16(w.y, a, b);
         h0[4] = a[0]; h0[5] = a[1]; h0[6] = b[0]; h0[7] = b[1];
-        i8x4_to_f16(w[2], a, b);
+        i8x4_to_f16(w.z, a, b);
         h1[0] = a[0]; h1[1] = a[1]; h1[2] = b[0]; h1[3] = b[1];
-        i8x4_to_f16(w[3], a, b);
+        i8x4_to_f16(w.w, a, b);
         h1[4] = a[0]; h1[5] = a[1]; h1[6] = b[0]; h1[7] = b[1];
         half8 *dst = (half8 *)((_Float16 *)buf + r * LDA + s * 16);
         dst[0] = h0;
@@ -431,11 +436,11 @@ __device__ __forceinline__ void a_store(const AReg &ar, char *buf, int item, flo
             sc[(s >> 1) * BM + r] = ar.d * unscale;
         }
     } else if constexpr (WT == W_F16) {
-        uint4 *dst = (uint4 *)((uint16_t *)buf + r * LDA + s * 16);
+        u32x4v *dst = (u32x4v *)((uint16_t *)buf + r * LDA + s * 16);
         dst[0] = ar.r[0];
         dst[1] = ar.r[1];
     } else {
-        uint4 *dst = (uint4 *)((float *)buf + r * LDA_F + s * 16);
+        u32x4v *dst = (u32x4v *)((float *)buf + r * LDA_F + s * 16);
         dst[0] = ar.r[0];
         dst[1] = ar.r[1];
         dst[2] = ar.r[2];
@@ -478,7 +483,7 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
 template <int WT, int NW, int BM, int NTW>
 struct MainloopPre {
     static constexpr int IT = (BM * (KC / 16) + NW * 64 - 1) / (NW * 64);
-    AReg ar[IT];
+    AReg<WT> ar[IT];
     WFrag<WT> wf[WT == W_F32 ? 1 : 2][NTW];
 };
 
@@ -521,7 +526,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
 #pragma unroll
         for (int j = 0; j < NTW; j++) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-    AReg ar[IT];
+    AReg<WT> ar[IT];
 #pragma unroll
     for (int it = 0; it < IT; it++) {
         const int item = tid + it * NT;
@@ -664,9 +669,9 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
-    // Q4 GELU: transposed accumulators in block-8 column order, epilogue in
-    // registers (gemm_gelu_blk8); otherwise 16-row LDS slices
-    constexpr bool GELU_T = QP && EPI == EPI_GELU_ACT;
+    // Q4 / F16 GELU: transposed accumulators (Q4: in block-8 column order,
+    // gemm_gelu_blk8), epilogue in registers; otherwise 16-row LDS slices
+    constexpr bool GELU_T = (QP || WT == W_F16) && EPI == EPI_GELU_ACT;
     // LN: two 16-row slice buffers (stage + row partials) for BN <= 768
     constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || GELU_T) ? 0 : (EPI == EPI_LN && BN <= 768 ? 2 : 1) * (16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0));
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
@@ -709,23 +714,43 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
             gemm_mainloop<WT, NW, BM, NTW, true>(args, m0, (n0 + wv * WN) >> 4, smem, acc, pre);
             const int64_t mc = m0;
             const int nc = n0;
-            // Transposed accumulators over W repacked in block-8 order
-            // (gemm_gelu_blk8): lane (g, c16) holds acc[rt][2p + t][i] =
-            // C[mc + 16 rt + c16][32 pb + 8 g + 4 t + i] (pb = the pair's
-            // 32-column block), i.e. one quarter of one row's Q8 block.
 #pragma unroll
             for (int p = 0; p < NP; p++) {
                 const int col = nc + wv * WN + 32 * p + 8 * g;
                 const float4v b0 = *(const float4v *)(args.bias + col), b1 = *(const float4v *)(args.bias + col + 4);
+                if constexpr (QP) {
+                    // Transposed accumulators over W repacked in block-8 order
+                    // (gemm_gelu_blk8): lane (g, c16) holds acc[rt][2p + t][i] =
+                    // C[mc + 16 rt + c16][32 pb + 8 g + 4 t + i] (pb = the pair's
+                    // 32-column block), i.e. one quarter of one row's Q8 block.
 #pragma unroll
-                for (int rt = 0; rt < RT; rt++) {
-                    float y[8];
+                    for (int rt = 0; rt < RT; rt++) {
+                        float y[8];
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        y[i] = h2f(gtab[f2h(fmaxf(b0[i] + acc[rt][2 * p][i], xlo))]);
-                        y[4 + i] = h2f(gtab[f2h(fmaxf(b1[i] + acc[rt][2 * p + 1][i], xlo))]);
+                        for (int i = 0; i < 4; i++) {
+                            y[i] = h2f(gtab[f2h(fmaxf(b0[i] + acc[rt][2 * p][i], xlo))]);
+                            y[4 + i] = h2f(gtab[f2h(fmaxf(b1[i] + acc[rt][2 * p + 1][i], xlo))]);
+                        }
+                        store_act_quarter_t<WT>(args.out_act, args.N, mc + rt * 16 + c16, col >> 5, g, y);
                     }
-                    store_act_quarter_t<WT>(args.out_act, args.N, mc + rt * 16 + c16, col >> 5, g, y);
+                } else {
+                    // F16 (plain pair-interleaved tile order, kernels.h WPtr): lane
+                    // (g, c16) holds acc[rt][2p + t][i] = C[mc + 16 rt + c16][32 pb +
+                    // 8 g + 2 i + t]: eight adjacent fp16 outputs, one 16-byte store.
+                    // ggml's gelu output is the table's fp16 value, stored as is.
+                    const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+                    for (int rt = 0; rt < RT; rt++) {
+                        uint4 pk;
+                        uint32_t *pw = (uint32_t *)&pk;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const uint32_t h0 = gtab[f2h(fmaxf(bb[2 * i] + acc[rt][2 * p][i], xlo))];
+                            const uint32_t h1 = gtab[f2h(fmaxf(bb[2 * i + 1] + acc[rt][2 * p + 1][i], xlo))];
+                            pw[i] = h0 | (h1 << 16);
+                        }
+                        *(uint4 *)((uint16_t *)args.out_act.q + (mc + rt * 16 + c16) * args.N + col) = pk;
+                    }
                 }
             }
             if (t + (int)gridDim.x < nwg) {
@@ -1692,7 +1717,7 @@ template <int WT, int EPI, int BN, int NW, int BM>
 static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
     const int mt = Mpad / BM, nt = a.N / BN;
     int grid = mt * nt;
-    if constexpr ((WT == W_Q4_0 || WT == W_Q4_1) && EPI == EPI_GELU_ACT) {
+    if constexpr ((WT == W_Q4_0 || WT == W_Q4_1 || WT == W_F16) && EPI == EPI_GELU_ACT) {
         // persistent: one workgroup per CU (the GELU table fills the LDS), a multiple of 8
         if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS) return hipErrorInvalidValue;
         grid = std::min(grid, std::max(8, n_cus() / 8 * 8));
@@ -1714,7 +1739,9 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
                                   : gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
         if (epi == EPI_LN && a.N == 384) return gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
-    } else if constexpr (WT == W_F16) {  // tools/gemm_bench: 12-wave 384-column tiles win by 1.4-1.9x
+    } else if constexpr (WT == W_F16) {
+        // tools/gemm_bench (e5 shapes): 12-wave 384-column tiles win by 1.3-1.8x over
+        // 4-6 waves and by 11-14 % over 768 x 64 tiles (qkv 343 us, up+GELU 368 us)
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_GELU_ACT)
             return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)

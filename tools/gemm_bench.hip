@@ -144,6 +144,12 @@ int main(int argc, char **argv) {
         GemmArgs u2 = g; u2.K = 768; u2.N = 3072;
         GemmArgs d2 = g; d2.K = 3072; d2.N = 768;
         const int M2 = 65536;
+        run<W_F16, EPI_QKV, 768, 12, 64>("f16 qkv <768,12,64>", q2, M2, iters);
+        run<W_F16, EPI_GELU_ACT, 768, 12, 64>("f16 up <768,12,64>", u2, M2, iters);
+        run<W_F16, EPI_QKV, 512, 8, 64>("f16 qkv <512,8,64>", q2, M2, iters);
+        run<W_F16, EPI_GELU_ACT, 512, 8, 64>("f16 up <512,8,64>", u2, M2, iters);
+        run<W_F16, EPI_NONE, 768, 12, 64>("f16 up NONE <768,12,64>", u2, M2, iters);
+        run<W_F16, EPI_NONE, 384, 12, 128>("f16 up NONE <384,12,128>", u2, M2, iters);
         run<W_F16, EPI_QKV, 384, 6, 64>("f16 qkv <384,6,64>", q2, M2, iters);
         run<W_F16, EPI_QKV, 384, 12, 128>("f16 qkv <384,12,128>", q2, M2, iters);
         run<W_F16, EPI_QKV, 256, 4, 128>("f16 qkv <256,4,128>", q2, M2, iters);
