@@ -972,16 +972,17 @@ __device__ __forceinline__ void attn_pv(float16v *o, const _Float16 *Vh, const _
     }
 }
 
-// The same with P given as the table's fp16 values (two 8-key halves).
-template <int D>
+// The same with P given as the table's fp16 values (two 8-key halves), for
+// NDT 32-dim blocks starting at block dt0.
+template <int D, int NDT = D / 32>
 __device__ __forceinline__ void attn_pv_h(float16v *o, const _Float16 *Vh, const _Float16 *Vl, int vst, int k0, int r,
-                                          int hh, const half8 (&ph)[2]) {
+                                          int hh, const half8 (&ph)[2], int dt0 = 0) {
 #pragma unroll
     for (int ks = 0; ks < 2; ks++) {
         const int key = k0 + 16 * ks + 4 * hh;
 #pragma unroll
-        for (int dt = 0; dt < D / 32; dt++) {
-            const int off = (dt * 32 + r) * vst + key;
+        for (int dt = 0; dt < NDT; dt++) {
+            const int off = ((dt0 + dt) * 32 + r) * vst + key;
             const half4v h0 = *(const half4v *)&Vh[off], h1 = *(const half4v *)&Vh[off + 8];
             const half4v l0 = *(const half4v *)&Vl[off], l1 = *(const half4v *)&Vl[off + 8];
             const half8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
@@ -994,16 +995,17 @@ __device__ __forceinline__ void attn_pv_h(float16v *o, const _Float16 *Vh, const
 
 // ctx = o * (float)(1/sum), stored in the O-projection's activation format:
 // lane (r, hh) holds ctx[row][h D + 32 dt + (j & 3) + 8 (j >> 2) + 4 hh], one
-// 32-value quant block per (query, dt) split over the lane pair (r, hh).
-template <int WT, int D>
+// 32-value quant block per (query, dt) split over the lane pair (r, hh); NDT
+// blocks from block dt0.
+template <int WT, int D, int NDT = D / 32>
 __device__ __forceinline__ void attn_store_ctx(const AttnArgs &a, float16v *o, float rs, int64_t row, bool valid,
-                                               int h, int hh) {
+                                               int h, int hh, int dt0 = 0) {
     const int E = a.E;
 #pragma unroll
-    for (int dt = 0; dt < D / 32; dt++) {
+    for (int dt = 0; dt < NDT; dt++) {
 #pragma unroll
         for (int j = 0; j < 16; j++) o[dt][j] *= rs;
-        const int col0 = h * D + dt * 32;
+        const int col0 = h * D + (dt0 + dt) * 32;
         if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
             float amax = 0.f;
 #pragma unroll
@@ -1189,27 +1191,33 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 }
 
 // QKV projection fused with attention, for batches whose sentences all have
-// n <= 128 tokens and heads of D = 32 (MiniLM): one 12-wave workgroup per
-// sentence, so Q, K and V (hi/lo, 4 bytes a value) never leave the CU —
-// the unfused pair writes and re-reads 12 bytes per token and feature.
-// Heads go four at a time (qkv_attention_ntw) through the GEMM main loop (one
-// n-tile per wave and head pair) and two at a time through the attention tiles: the main loop (gemm_mainloop, the 128 rows
-// from the sentence's first token) computes the pair's 192 head-major QKV
-// features (kernels.h GemmArgs), one 16-feature n-tile per wave; b + W.x is
-// split hi/lo into the two heads' attention tiles in LDS, and the 8
-// (head, 32-query) attention tasks run as in attention_short_kernel.
-constexpr int QKVA_NW = 12, QKVA_D = 32;  // waves, head dim
+// n <= 128 tokens, heads of D = 32 (MiniLM) or 64 (e5-base, bge-large): one
+// 12-wave workgroup per sentence, so Q, K and V (hi/lo, 4 bytes a value)
+// never leave the CU — the unfused pair writes and re-reads 12 bytes per
+// token and feature.  The QKV features go through the GEMM main loop in
+// 192-feature units (a head pair at D = 32, one head at D = 64), NTW units per
+// main loop (qkv_attention_ntw) and one unit at a time through the attention
+// tiles: the main loop (gemm_mainloop, the 128 rows from the sentence's first
+// token) computes the unit's head-major QKV features (kernels.h GemmArgs), one
+// 16-feature n-tile per wave; b + W.x is split hi/lo into the unit's attention
+// tiles in LDS, and 8 attention tasks of 32 queries run as in
+// attention_short_kernel: (head, query block) at D = 32, (query block, 32-dim
+// half of the context) at D = 64 (the two halves share the scores, computed
+// by both waves).
+constexpr int QKVA_NW = 12;  // waves
 
-// NTW: head pairs per main loop (qkv_attention_ntw); PK: sentence tiles (a.tiles)
-template <int WT, int NTW, bool PK>
+// D: head dim; NTW: 192-feature units per main loop (qkv_attention_ntw); PK:
+// sentence tiles (a.tiles)
+template <int WT, int D, int NTW, bool PK>
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
-    constexpr int D = QKVA_D, NW = QKVA_NW, BM = 128, RT = BM / 16;
+    constexpr int NW = QKVA_NW, BM = 128, RT = BM / 16;
+    constexpr int HU = 192 / (3 * D);  // heads per unit
     constexpr int NK = 128, KST = D + 8, VST = NK + 4;
     constexpr int A_BUF = (WT == W_F32 ? BM * LDA_F * 4 : BM * LDA_H * 2) + (QP ? KB * BM * 4 : 0);
     constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
-    constexpr int SMEM = (2 * A_BUF > 2 * SLOT) ? 2 * A_BUF : 2 * SLOT;
-    static_assert(NW * 16 == 2 * 3 * D, "one 16-feature n-tile per wave covers a head pair");
+    constexpr int SMEM = (2 * A_BUF > HU * SLOT) ? 2 * A_BUF : HU * SLOT;
+    static_assert(NW * 16 == HU * 3 * D, "one 16-feature n-tile per wave covers a unit");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     // PK: a workgroup owns a tile of ns <= 4 consecutive sentences (AttnArgs.tiles:
@@ -1259,20 +1267,21 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     };
     int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
     asm volatile("" : "+v"(lim));
-    // wave w: n-tile w of the pair = features 16 w .. 16 w + 15 of the pair's
+    // wave w: n-tile w of the unit = features 16 w .. 16 w + 15 of the unit's
     // range (g.W is this kernel's own copy of the head-major QKV weights, in
-    // plain tile order), i.e. head slot w / 6, part (w % 6) / 2, head dims
-    // d0 .. d0 + 15 with d0 = 16 (w % 2).  Q and K waves run the transposed main
-    // loop (a lane holds one row x four adjacent dims: 8-byte stores into the
-    // row-major Q / K tiles), V waves the plain one (one dim x four adjacent
-    // rows: 8-byte stores into V^T).
-    const int hs_w = wv / 6, part_w = (wv % 6) / 2, d0 = 16 * (wv & 1);
+    // plain tile order), i.e. head slot w / (3 D / 16), part (Q, K, V), head
+    // dims d0 .. d0 + 15.  Q and K waves run the transposed main loop (a lane
+    // holds one row x four adjacent dims: 8-byte stores into the row-major Q / K
+    // tiles), V waves the plain one (one dim x four adjacent rows: 8-byte
+    // stores into V^T).
+    constexpr int WPH = 3 * D / 16;  // waves per head
+    const int hs_w = wv / WPH, part_w = (wv % WPH) / (D / 16), d0 = 16 * (wv & (D / 16 - 1));
 
-    for (int qd = 0; qd < a.H / (2 * NTW); qd++) {
-        // heads 2 NTW qd ..: one main loop (one pass over the sentence's A panel)
-        // serves NTW head pairs.  g.W is in grouped tile order (runtime.cpp): wave
-        // w's n-tiles nt0 + t are n-tile w of pair NTW qd + t, so acc[..][half]
-        // plays the one-pair role of the split below.
+    for (int qd = 0; qd < a.H / (HU * NTW); qd++) {
+        // units NTW qd ..: one main loop (one pass over the sentence's A panel)
+        // serves NTW units.  g.W is in grouped tile order (runtime.cpp): wave
+        // w's n-tiles nt0 + t are n-tile w of unit NTW qd + t, so acc[..][half]
+        // plays the one-unit role of the split below.
         const int64_t nt0 = (int64_t)qd * NTW * NW + NTW * wv;
         float4v acc[RT][NTW];
         MainloopPre<WT, NW, BM, NTW> pre;
@@ -1284,7 +1293,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 #pragma unroll
         for (int half = 0; half < NTW; half++) {
             const int pr = NTW * qd + half;
-            const int fpair = pr * 6 * D;  // first head-major feature of the pair
+            const int fpair = pr * (HU * 3 * D);  // first head-major feature of the unit
             {   // y = b + W.x -> hi / lo attention tiles (rows >= n: zero keys and values).
                 // LDS byte offsets and row limits are rebuilt per pair behind opaque
                 // moves, so the compiler does not hoist addresses / row masks out of
@@ -1352,8 +1361,9 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
             }
             __syncthreads();
 
-            if (wv < 8) {  // attention task (head slot, query block: 32 queries of one sentence)
-                const int hs = wv >> 2, qb = wv & 3, head = 2 * pr + hs;
+            if (wv < 8) {  // attention task (head slot or dim half, query block: 32 queries of one sentence)
+                const int hs = HU == 2 ? wv >> 2 : 0, qb = wv & 3, head = HU * pr + hs;
+                const int dh = HU == 2 ? 0 : wv >> 2;  // D = 64: the 32-dim half of the context
                 int kb = 0, len = n, qrel = 32 * qb, vs = 0;
                 if constexpr (PK) {
                     kb = qtab[qb][0];
@@ -1405,9 +1415,8 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     // multiple of 2^-24 in [0, 1], so p * 2^24 is an integer and the
                     // sum of n <= 128 of them fits a uint32
                     uint32_t sum = 0;
-                    float16v o[D / 32];
-#pragma unroll
-                    for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
+                    float16v o[1];
+                    o[0] = float16v{};
                     for (int kt = 0; kt < nkt; kt++) {
                         const float16v S = scores(kt);
                         half8 ph[2];
@@ -1421,10 +1430,11 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                             ph[j >> 3][j & 7] = __builtin_bit_cast(_Float16, pb);
                             sum += (uint32_t)(h2f(pb) * 16777216.0f);
                         }
-                        attn_pv_h<D>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph);
+                        attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph, dh);
                     }
                     sum += __shfl_xor(sum, 32);
-                    attn_store_ctx<WT, D>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + qrow, qrel + r < len, head, hh);
+                    attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + qrow, qrel + r < len, head,
+                                             hh, dh);
                 }
             }
             __syncthreads();  // the next pair's tiles / the next quad's A chunks overwrite the attention tiles
@@ -1432,21 +1442,30 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     }
 }
 
-template <int WT>
+template <int WT, int D>
 static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
     const bool pk = a.tiles != nullptr;
     if (qkv_attention_ntw(WT) == 2) {
         if (pk)
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, 2, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
         else
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, 2, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
     } else {
         if (pk)
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, 1, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
         else
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, 1, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
     }
     return hipGetLastError();
+}
+
+template <int WT>
+static hipError_t qkv_attn_w(const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
+    switch (a.H > 0 ? a.E / a.H : 0) {
+        case 32: return qkv_attn_t<WT, 32>(g, a, n_blocks, s);
+        case 64: return qkv_attn_t<WT, 64>(g, a, n_blocks, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 // Head pairs per main loop: two (one pass over a sentence's A panel serves
@@ -1482,15 +1501,17 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles) {
 }
 
 bool qkv_attention_supported(int wtype, int E, int H, int max_len) {
-    return max_len <= 128 && E / H == QKVA_D && H % (2 * qkv_attention_ntw(wtype)) == 0 && E % KC == 0 &&
-           wtype != W_F32;
+    if (H <= 0 || E % H) return false;
+    const int D = E / H;
+    return max_len <= 128 && (D == 32 || D == 64) && H % (192 / (3 * D) * qkv_attention_ntw(wtype)) == 0 &&
+           E % KC == 0 && wtype != W_F32;
 }
 
 hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
     switch (wtype) {
-        case W_F16: return qkv_attn_t<W_F16>(g, a, n_blocks, s);
-        case W_Q4_0: return qkv_attn_t<W_Q4_0>(g, a, n_blocks, s);
-        case W_Q4_1: return qkv_attn_t<W_Q4_1>(g, a, n_blocks, s);
+        case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, s);
+        case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, s);
+        case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, s);
     }
     return hipErrorInvalidValue;
 }

@@ -912,9 +912,10 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
             // undo repack's column interleave (row 32p + 2c + t <- 32p + 16t + c) so
             // that repacked tile j holds features 16j .. 16j + 15 in order
             // after the grouped tile order (kernels.hip qkv_attention_kernel): tile
-            // G tpp q + G w + t <- n-tile w of head pair G q + t (tpp n-tiles per
-            // pair, G = pairs per main loop; G = 1 is the plain order)
-            const size_t tpp = (size_t)(6 * Dh / 16), G = (size_t)qkv_attention_ntw(ctx->wtype);
+            // G tpp q + G w + t <- n-tile w of 192-feature unit G q + t (tpp = 12
+            // n-tiles per unit: a head pair at head dim 32, one head at 64; G =
+            // units per main loop; G = 1 is the plain order)
+            const size_t tpp = 12, G = (size_t)qkv_attention_ntw(ctx->wtype);
             std::vector<const uint8_t *> quad(rows.size()), plain(rows.size());
             for (size_t T = 0; T < rows.size() / 16; T++) {
                 const size_t src = tpp * (G * (T / (G * tpp)) + T % G) + (T % (G * tpp)) / G;

@@ -44,6 +44,9 @@ CASES = {
     "c4_e5_f16": ("e5-base", "f16", 0.05, [256, 256]),
     "c5_bge_q4_1": ("bge-large", "q4_1", 0.05, [512, 512]),
     "c5_bge_q4_1_l2": ("bge-large", "q4_1", 0.05, [512, 77], 2),
+    # short sentences on the head-dim-64 shapes: the fused QKV + attention kernel
+    "c4_e5_f16_short": ("e5-base", "f16", 0.05, [1, 7, 33, 64, 100, 128]),
+    "c5_bge_q4_1_l2_short": ("bge-large", "q4_1", 0.05, [5, 40, 128], 2),
 }
 
 # Cases whose Q8 re-quantisation amplifies ANY f32-level rounding difference

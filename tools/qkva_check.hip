@@ -96,9 +96,9 @@ int main() {
         CK(hipMemset(ctx, 0xff, (size_t)Mpad * E * 2));
         a.ctx.q = ctx;
         if (G == 1)
-            hipLaunchKernelGGL((qkv_attention_kernel<W_F16, 1, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<W_F16, 32, 1, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
         else
-            hipLaunchKernelGGL((qkv_attention_kernel<W_F16, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<W_F16, 32, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
         CK(hipGetLastError());
         CK(hipDeviceSynchronize());
         out[G - 1].resize((size_t)M * E);

@@ -90,7 +90,7 @@ int main(int argc, char **argv) {
     for (int K : {E, 0}) {
         g.K = K;
         auto launch = [&] {
-            hipLaunchKernelGGL((qkv_attention_kernel<W_Q4_0, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<W_Q4_0, 32, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
         };
         for (int i = 0; i < 3; i++) launch();
         CK(hipGetLastError());
