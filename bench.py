@@ -332,6 +332,25 @@ def main():
         log("variable-length batch timing")
         ragged = ragged_line(8, 128, 0)
         ragged_short = ragged_line(8, 40, 1)
+        # the same 8..128 batch through bert_eval_batch on host buffers: the
+        # library may reorder it (fused-kernel tile packing), outputs per sentence
+        rng = np.random.default_rng(SEED + rank)
+        lens = rng.integers(8, 129, B)
+        rtoks = [toks[i][:n].copy() for i, n in enumerate(lens)]
+        for t in rtoks:
+            t[-1] = 102
+        run, remb = model.prepared_batch(rtoks)
+        for _ in range(2):
+            run()
+        ts = []
+        for _ in range(max(3, args.host_runs)):
+            t0 = time.perf_counter()
+            run()
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        ragged["host_api"] = dict(value=round(B / med, 1), unit="embeddings/s", ms_median=round(med * 1e3, 3),
+                                  unit_norm=bool(np.allclose(np.linalg.norm(remb, axis=1), 1.0, atol=1e-5)),
+                                  note="bert_eval_batch, host buffers, same lengths")
 
     cpu = None
     parity = None

@@ -1200,6 +1200,35 @@ bool eval_host_slice(bert_ctx *ctx, Replica &R, bert_vocab_id **toks, const int3
 
 void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs);
 
+// Order for sentences of <= 128 tokens that lets the fused kernel's
+// consecutive packing (run_pipeline) fill its 128-row tiles: first-fit
+// decreasing on the lengths rounded up to 32 (classes 128, 96, 64, 32), each
+// bin's sentences adjacent: 128 alone, 96 + 32, 64 + 64, 64 + 32 + 32, 4 x 32.
+// Results do not depend on the order (packed sentences are bitwise equal to
+// the sentence alone), and the caller's output rows are addressed per sentence.
+std::vector<int> tile_order(const int32_t *ntok, const std::vector<int> &idx) {
+    std::vector<int> cls[4];  // span 32, 64, 96, 128
+    for (int s : idx) cls[std::min(3, (ntok[s] - 1) >> 5)].push_back(s);
+    std::vector<int> out;
+    out.reserve(idx.size());
+    size_t i32 = 0;
+    for (int s : cls[3]) out.push_back(s);
+    for (int s : cls[2]) {
+        out.push_back(s);
+        if (i32 < cls[0].size()) out.push_back(cls[0][i32++]);
+    }
+    for (size_t k = 0; k < cls[1].size(); k += 2) {
+        out.push_back(cls[1][k]);
+        if (k + 1 < cls[1].size()) {
+            out.push_back(cls[1][k + 1]);
+        } else {
+            for (int j = 0; j < 2 && i32 < cls[0].size(); j++) out.push_back(cls[0][i32++]);
+        }
+    }
+    while (i32 < cls[0].size()) out.push_back(cls[0][i32++]);
+    return out;
+}
+
 // Host-pointer batch eval, sharded over the context's replicas by token count.
 void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
     if (!ctx || n <= 0 || !toks || !ntok || !embs) return;
@@ -1224,24 +1253,26 @@ void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *nt
     // (short sentences, then the rest), so one long sentence does not move
     // every short one onto the unfused pair.  Sentences are independent, so
     // the results do not depend on the grouping.
+    // The short sentences are also put in tile order (tile_order) so that they
+    // share fused-kernel workgroups.
     const HParams &hp = ctx->hp;
     if (qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, GEMM_BM)) {
         std::vector<int> shrt, lng;
         for (int s = 0; s < n; s++) (ntok[s] <= GEMM_BM ? shrt : lng).push_back(s);
-        if (!shrt.empty() && !lng.empty()) {
-            for (const std::vector<int> *grp : {&shrt, &lng}) {
-                std::vector<bert_vocab_id *> t;
-                std::vector<int32_t> c;
-                std::vector<float *> e;
-                for (int s : *grp) {
-                    t.push_back(toks[s]);
-                    c.push_back(ntok[s]);
-                    e.push_back(embs[s]);
-                }
-                dispatch_batch(ctx, (int32_t)grp->size(), t.data(), c.data(), e.data());
+        shrt = tile_order(ntok, shrt);
+        for (const std::vector<int> *grp : {&shrt, &lng}) {
+            if (grp->empty()) continue;
+            std::vector<bert_vocab_id *> t;
+            std::vector<int32_t> c;
+            std::vector<float *> e;
+            for (int s : *grp) {
+                t.push_back(toks[s]);
+                c.push_back(ntok[s]);
+                e.push_back(embs[s]);
             }
-            return;
+            dispatch_batch(ctx, (int32_t)grp->size(), t.data(), c.data(), e.data());
         }
+        return;
     }
     dispatch_batch(ctx, n, toks, ntok, embs);
 }
