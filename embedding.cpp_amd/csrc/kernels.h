@@ -159,7 +159,12 @@ bool qkv_attention_supported(int wtype, int E, int H, int max_len);
 int qkv_attention_ntw(int wtype);
 // n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
 hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s);
-hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s);
+// out_row (optional): output row of each sentence (default: its batch index)
+hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s,
+                       const int32_t *out_row = nullptr);
+// dst = the batch's token ids with sentence i taken from sentence perm[i]
+hipError_t launch_gather_tokens(const int32_t *src, const int32_t *src_off, const int32_t *perm, const int32_t *dst_off,
+                                int32_t *dst, int n_seqs, hipStream_t s);
 hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const float *b, float eps,
                      const ActPtr &out, hipStream_t s);
 bool gemm_shape_supported(int epi, int N, int K);

@@ -1674,7 +1674,9 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
 // sum of squares in double, sqrtf, 1.0f/len, scale (:1002-1006).  One thread
 // per 4 columns; the token loop is unrolled 8-deep so loads are in flight
 // together (the fma chain per column stays in token order).
-__global__ __launch_bounds__(256) void pool_l2_kernel(const float *X, const int32_t *offsets, int E, float *out) {
+// out_row (optional): the output row of each sentence of the batch.
+__global__ __launch_bounds__(256) void pool_l2_kernel(const float *X, const int32_t *offsets, int E, float *out,
+                                                      const int32_t *out_row) {
     __shared__ double red[4];
     const int s = blockIdx.x, tid = threadIdx.x, c = 4 * tid;
     const int beg = offsets[s], n = offsets[s + 1] - beg;
@@ -1707,7 +1709,18 @@ __global__ __launch_bounds__(256) void pool_l2_kernel(const float *X, const int3
     const double tot = red[0] + red[1] + red[2] + red[3];
     const float len = sqrtf((float)tot);
     const float r = 1.0f / len;
-    if (c < E) *(float4v *)(out + (int64_t)s * E + c) = float4v{acc[0] * r, acc[1] * r, acc[2] * r, acc[3] * r};
+    const int64_t orow = out_row ? out_row[s] : s;
+    if (c < E) *(float4v *)(out + orow * E + c) = float4v{acc[0] * r, acc[1] * r, acc[2] * r, acc[3] * r};
+}
+
+// Token ids of a batch in a new sentence order: sentence i of the new batch
+// is sentence perm[i] of the caller's (one workgroup per sentence).
+__global__ __launch_bounds__(128) void gather_tokens_kernel(const int32_t *__restrict__ src, const int32_t *__restrict__ src_off,
+                                                            const int32_t *__restrict__ perm,
+                                                            const int32_t *__restrict__ dst_off, int32_t *__restrict__ dst) {
+    const int i = blockIdx.x, s = perm[i];
+    const int b = src_off[s], n = src_off[s + 1] - b, d = dst_off[i];
+    for (int t = threadIdx.x; t < n; t += 128) dst[d + t] = src[b + t];
 }
 
 // ---------------------------------------------------------------------------
@@ -1867,9 +1880,16 @@ hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s) {
+hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s,
+                       const int32_t *out_row) {
     if (E > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pool_l2_kernel, dim3(n_seqs), dim3(256), 0, s, X, offsets, E, out);
+    hipLaunchKernelGGL(pool_l2_kernel, dim3(n_seqs), dim3(256), 0, s, X, offsets, E, out, out_row);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_tokens(const int32_t *src, const int32_t *src_off, const int32_t *perm, const int32_t *dst_off,
+                                int32_t *dst, int n_seqs, hipStream_t s) {
+    hipLaunchKernelGGL(gather_tokens_kernel, dim3(n_seqs), dim3(128), 0, s, src, src_off, perm, dst_off, dst);
     return hipGetLastError();
 }
 

@@ -189,6 +189,7 @@ struct Workspace {
     ActPtr Xa, Ca, Ua;
     int32_t *tok = nullptr, *off = nullptr, *rowpos = nullptr;
     int32_t *tiles = nullptr;  // qkv_attention_kernel's sentence tiles: [first, count] pairs
+    int32_t *perm = nullptr;   // eval_device in tile order: caller's index of each sentence
     std::vector<int32_t> h_tiles;
     std::vector<void *> allocs;
     // pinned host staging for the host-pointer ABI
@@ -459,7 +460,7 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, h
     w.X = w.out = nullptr;
     w.qk_hi = w.qk_lo = w.vt_hi = w.vt_lo = nullptr;
     w.Xa = w.Ca = w.Ua = ActPtr{};
-    w.tok = w.off = w.rowpos = w.tiles = nullptr;
+    w.tok = w.off = w.rowpos = w.tiles = w.perm = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const int wt = ctx->wtype;
     if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
@@ -468,7 +469,8 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, h
         !alloc_act(w.allocs, w.Xa, wt, rows, E, st) || !alloc_act(w.allocs, w.Ca, wt, rows, E, st) ||
         !alloc_act(w.allocs, w.Ua, wt, rows, I, st) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
         !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4) ||
-        !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4) || !dmalloc(w.allocs, &w.tiles, (size_t)seqs * 2 * 4))
+        !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4) || !dmalloc(w.allocs, &w.tiles, (size_t)seqs * 2 * 4) ||
+        !dmalloc(w.allocs, &w.perm, (size_t)seqs * 4))
         return false;
     // padding rows must hold finite values: zero everything once
     HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, st));
@@ -694,8 +696,9 @@ EmbedArgs embed_args(const bert_ctx *ctx, Replica &R, const int32_t *d_tok, cons
 }
 
 // The fixed pipeline over a ragged batch already resident on the device.
+// d_out_row (optional): output row of each sentence of the batch.
 bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
-                  int n_seqs, float *d_out, hipStream_t st) {
+                  int n_seqs, float *d_out, hipStream_t st, const int32_t *d_out_row = nullptr) {
     const HParams &hp = ctx->hp;
     const int64_t M = h_off[n_seqs];
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
@@ -794,7 +797,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         HIP_OK(hipEventRecord(R.ev_join, R.stream2));
         HIP_OK(hipStreamWaitEvent(st, R.ev_join, 0));
     }
-    LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st));
+    LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st, d_out_row));
     return true;
 }
 
@@ -1229,6 +1232,19 @@ std::vector<int> tile_order(const int32_t *ntok, const std::vector<int> &idx) {
     return out;
 }
 
+// Workgroups run_pipeline's consecutive packing makes of sentences in `order`.
+int greedy_tiles(const int32_t *ntok, const std::vector<int> &order) {
+    int tiles = 0;
+    for (size_t i = 0; i < order.size();) {
+        int used = (ntok[order[i]] + 31) & ~31;
+        size_t k = i + 1;
+        while (k < order.size() && used + ((ntok[order[k]] + 31) & ~31) <= GEMM_BM) used += (ntok[order[k++]] + 31) & ~31;
+        tiles++;
+        i = k;
+    }
+    return tiles;
+}
+
 // Host-pointer batch eval, sharded over the context's replicas by token count.
 void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
     if (!ctx || n <= 0 || !toks || !ntok || !embs) return;
@@ -1502,6 +1518,38 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
     // stream, which is ordered with the caller's other work on it
     const hipStream_t st = (hipStream_t)hip_stream;
     try {
+        // Short sentences in the caller's order may leave fused-kernel tiles
+        // half empty: when the tile order (tile_order) needs fewer workgroups,
+        // the batch is gathered into that order on the device and each
+        // embedding is written back to its caller row (results unchanged).
+        const HParams &hp = ctx->hp;
+        std::vector<int32_t> ntok(n_seqs);
+        int max_len = 0;
+        for (int s = 0; s < n_seqs; s++) max_len = std::max(max_len, ntok[s] = h_offsets[s + 1] - h_offsets[s]);
+        if (n_seqs > 1 && qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, max_len)) {
+            std::vector<int> idx(n_seqs);
+            for (int s = 0; s < n_seqs; s++) idx[s] = s;
+            const std::vector<int> order = tile_order(ntok.data(), idx);
+            const int t_order = greedy_tiles(ntok.data(), order);
+            if (t_order < greedy_tiles(ntok.data(), idx) && qkv_attention_pack_pays(n_seqs, t_order)) {
+                const int64_t M = h_offsets[n_seqs];
+                const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
+                if (!ensure_workspace(ctx, R, Mpad, n_seqs, st)) return -4;
+                Workspace &w = R.ws;
+                std::vector<int32_t> off2(n_seqs + 1), perm(order.begin(), order.end());
+                off2[0] = 0;
+                for (int i = 0; i < n_seqs; i++) off2[i + 1] = off2[i] + ntok[order[i]];
+                // pageable sources: staged before the calls return
+                if (hipMemcpyAsync(w.off, off2.data(), (size_t)(n_seqs + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipMemcpyAsync(w.perm, perm.data(), (size_t)n_seqs * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    launch_gather_tokens(d_tokens, d_offsets, w.perm, w.off, w.tok, n_seqs, st) != hipSuccess) {
+                    set_err("bert_amd_eval_device: reorder failed");
+                    return -4;
+                }
+                if (!run_pipeline(ctx, R, w.tok, w.off, off2.data(), n_seqs, d_out, st, w.perm)) return -4;
+                return 0;
+            }
+        }
         if (!run_pipeline(ctx, R, d_tokens, d_offsets, h_offsets, n_seqs, d_out, st)) return -4;
     } catch (const std::exception &e) {
         set_err("%s", e.what());

@@ -349,6 +349,35 @@ def test_packed_short_sentences_equal_alone(ftype, pack, model_dir, monkeypatch)
     assert c.min() >= COS_TOL, 1 - c
 
 
+def test_device_batch_reordered_into_tiles(model_dir):
+    """bert_amd_eval_device on a ragged short-sentence batch in an order that
+    packs badly: the library gathers it into tile order on the device and
+    writes every embedding back to the caller's row — equal, bitwise, to the
+    host ABI and to each sentence alone."""
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    rng = np.random.default_rng(77)
+    lens = np.tile([100, 20, 90, 30, 70, 60, 10, 128], 80)  # 640 sentences
+    toks = [[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in lens]
+    hip = Hip()
+    offs = np.zeros(len(toks) + 1, np.int32)
+    offs[1:] = np.cumsum(lens)
+    flat = np.concatenate([np.asarray(t, np.int32) for t in toks])
+    d_tok, d_off, d_out = hip.malloc(flat.nbytes), hip.malloc(offs.nbytes), hip.malloc(len(toks) * m.n_embd * 4)
+    try:
+        hip.h2d(d_tok, flat)
+        hip.h2d(d_off, offs)
+        m.eval_device(d_tok, d_off, offs, len(toks), d_out, 0)
+        hip.sync(0)
+        dev = np.empty((len(toks), m.n_embd), np.float32)
+        hip.d2h(dev, d_out)
+    finally:
+        for ptr in (d_tok, d_off, d_out):
+            hip.free(ptr)
+    assert np.array_equal(dev, m.eval_batch(toks))
+    for i in (0, 1, 6, 7, 333):
+        assert np.array_equal(dev[i], m.eval(toks[i])), i
+
+
 def test_fused_head_quads_equal_head_pairs():
     """qkv_attention_kernel with two head pairs per GEMM main loop (grouped
     weight tile order, the default) is bitwise identical to one pair per main
