@@ -322,6 +322,20 @@ def test_mixed_lengths_group_like_separate_batches(model_dir):
     assert np.array_equal(full[[1, 3, 5]], long_)
 
 
+def test_packed_head_dim_64_equal_alone(model_dir, monkeypatch):
+    """Packed fused tiles at head dim 64 (e5-base f16, packing forced): every
+    sentence equals itself evaluated alone, bitwise."""
+    p, m = get_model(model_dir, "e5-base", "f16")
+    rng = np.random.default_rng(5)
+    lens = [1, 3, 31, 32, 33, 64, 7, 90, 20, 128, 45, 12] * 4
+    toks = [[101] + rng.integers(1000, 250002, max(n - 2, 0)).tolist() + [102] if n >= 2 else [101] for n in lens]
+    monkeypatch.setenv("BERT_AMD_PACK", "1")
+    full = m.eval_batch(toks)
+    monkeypatch.setenv("BERT_AMD_PACK", "0")
+    bad = [i for i in range(len(toks)) if not np.array_equal(full[i], m.eval(toks[i]))]
+    assert not bad, [(i, lens[i]) for i in bad]
+
+
 @pytest.mark.parametrize("ftype", ["q4_0", "f16"])
 @pytest.mark.parametrize("pack", ["1", "auto"])
 def test_packed_short_sentences_equal_alone(ftype, pack, model_dir, monkeypatch):
