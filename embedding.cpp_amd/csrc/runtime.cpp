@@ -531,20 +531,29 @@ void drain_profile(Replica &R) {
 
 // Q4 models run selected projections on the int8-MFMA GEMMs (gemm_i8.hip:
 // 1 B/weight, exact isum per block on the int8 MFMA, d_w * d_a applied in
-// the kernel like ggml's vec_dot).  Default: the FFN-up GEMM only — there it
-// beats the split-fp16 GEMM in the pipeline; for the O and FFN-down
-// projections (LayerNorm epilogues) it does not.  Env
-// BERT_AMD_I8 (read at load): "0" none, "1" / "all" all three, "up" default.
+// the kernel like ggml's vec_dot).  Default: FFN-up (faster than the
+// split-fp16 GEMM) and FFN-down (as fast on full batches, faster on ragged
+// ones); the O projection stays on the split-fp16 GEMM.  Env
+// BERT_AMD_I8 (read at load): "0" none, "1" / "all" all three, or a comma list
+// of up, o, down.
 void i8_select(bert_ctx *ctx) {
     const char *e = std::getenv("BERT_AMD_I8");
-    const std::string v = e ? e : "up";
+    // default: FFN-up and FFN-down (tools/ab_bench.sh: down on int8 equals the split
+    // kernel on the full 1024 x 128 batch and is 3 % faster on ragged batches;
+    // o-proj on int8 is 20 % slower)
+    const std::string v = e ? e : "up,down";
     const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const bool q4 = ctx->wtype == W_Q4_0 || ctx->wtype == W_Q4_1;
     const int ln = E == 384 ? EPI_LN : EPI_RESID;
+    // "0": none, "1" / "all": every projection, else a comma list of up, o, down
     const bool all = v == "1" || v == "all";
-    ctx->i8_up = q4 && (all || v == "up") && i8_gemm_supported(EPI_GELU_ACT, I, E);
-    ctx->i8_o = q4 && all && i8_gemm_supported(ln, E, E);
-    ctx->i8_down = q4 && all && i8_gemm_supported(ln, E, I);
+    auto has = [&](const char *p) {
+        const std::string t = std::string(",") + v + ",";
+        return all || t.find(std::string(",") + p + ",") != std::string::npos;
+    };
+    ctx->i8_up = q4 && has("up") && i8_gemm_supported(EPI_GELU_ACT, I, E);
+    ctx->i8_o = q4 && has("o") && i8_gemm_supported(ln, E, E);
+    ctx->i8_down = q4 && has("down") && i8_gemm_supported(ln, E, I);
 }
 
 // One encoder layer over the row group [row0, row0 + rows) (sentences

@@ -108,14 +108,17 @@ def test_every_weight_type_vs_oracle(ftype, model_dir):
     assert c.min() >= COS_TOL, (ftype, 1 - c)
 
 
+@pytest.mark.parametrize("mode", ["1", "0"])
 @pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_1", "minilm_q4_0_std01"])
-def test_int8_gemm_path_golden(case, model_dir, monkeypatch):
-    """The opt-in int8-MFMA Q4 GEMMs (env BERT_AMD_I8=1: gemm_i8.hip, scales
-    applied in-kernel per block like ggml_vec_dot_q4_x_q8_x) against the same
-    golden fixtures, and bitwise deterministic."""
+def test_int8_gemm_path_golden(case, mode, model_dir, monkeypatch):
+    """Every Q4 projection on the int8-MFMA GEMMs (env BERT_AMD_I8=1:
+    gemm_i8.hip, scales applied in-kernel per block like
+    ggml_vec_dot_q4_x_q8_x), and every one on the split-fp16 GEMMs
+    (BERT_AMD_I8=0), against the same golden fixtures, bitwise deterministic
+    (the default mixes the two: up and down int8, o split-fp16)."""
     meta, toks, want = load_case(case)
     p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    monkeypatch.setenv("BERT_AMD_I8", "1")
+    monkeypatch.setenv("BERT_AMD_I8", mode)
     m = bertlib.BertModel(p)
     try:
         got = m.eval_batch(toks)
@@ -123,7 +126,7 @@ def test_int8_gemm_path_golden(case, model_dir, monkeypatch):
     finally:
         m.close()
     c = cos(got, want)
-    print(f"int8 {case}: 1-cos max {1 - c.min():.2e}")
+    print(f"BERT_AMD_I8={mode} {case}: 1-cos max {1 - c.min():.2e}")
     assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
 
 
