@@ -541,7 +541,9 @@ void i8_select(bert_ctx *ctx) {
     // default: FFN-up and FFN-down (tools/ab_bench.sh: down on int8 equals the split
     // kernel on the full 1024 x 128 batch and is 3 % faster on ragged batches;
     // o-proj on int8 is 20 % slower)
-    const std::string v = e ? e : "up,down";
+    // (the down GEMM only where its LayerNorm is fused, E = 384: wider rows use
+    // the int8 residual kernel + launch_ln, 8 % slower than split-fp16 on C5)
+    const std::string v = e ? e : (ctx->hp.n_embd == 384 ? "up,down" : "up");
     const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const bool q4 = ctx->wtype == W_Q4_0 || ctx->wtype == W_Q4_1;
     const int ln = E == 384 ? EPI_LN : EPI_RESID;
