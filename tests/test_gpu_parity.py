@@ -395,6 +395,26 @@ def test_device_batch_reordered_into_tiles(model_dir):
         assert np.array_equal(dev[i], m.eval(toks[i])), i
 
 
+@pytest.mark.parametrize("i8", ["default", "0"])
+def test_half_row_ln_tiles(i8, model_dir, monkeypatch):
+    """A batch whose 128-row LN GEMM tiles would leave the last round of
+    workgroups mostly empty runs 64-row tiles (kernels.hip ln_half_rows):
+    per-sentence results equal the sentences alone, bitwise."""
+    if i8 != "default":
+        monkeypatch.setenv("BERT_AMD_I8", i8)
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    m = bertlib.BertModel(p)  # fresh context: BERT_AMD_I8 is read at load
+    try:
+        rng = np.random.default_rng(11)
+        toks = [[101] + rng.integers(1000, 30522, 98).tolist() + [102] for _ in range(400)]  # 40 000 rows
+        full = m.eval_batch(toks)
+        assert np.allclose(np.linalg.norm(full, axis=1), 1.0, atol=1e-5)
+        for i in (0, 1, 255, 399):
+            assert np.array_equal(full[i], m.eval(toks[i])), i
+    finally:
+        m.close()
+
+
 def test_fused_head_quads_equal_head_pairs():
     """qkv_attention_kernel with two head pairs per GEMM main loop (grouped
     weight tile order, the default) is bitwise identical to one pair per main
