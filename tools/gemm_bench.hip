@@ -29,6 +29,46 @@ static void *dev_random(size_t bytes, uint32_t seed, int kind) {
     return d;
 }
 
+// main loop only, transposed or plain MFMA form (the fused kernel's Q/K waves
+// run the transposed form, its V waves the plain one)
+template <int WT, int NW, int BM, int NTW, bool TRANS>
+__global__ __launch_bounds__(NW * 64) void mainloop_probe(GemmArgs args, int n_ntiles) {
+    constexpr int A_BUF = BM * LDA_H * 2 + KB * BM * 4;
+    __shared__ __attribute__((aligned(16))) char smem[2 * A_BUF];
+    const int mt = blockIdx.x / n_ntiles, nt = blockIdx.x % n_ntiles;
+    const int64_t m0 = (int64_t)mt * BM, ntile0 = (int64_t)nt * NW * NTW + NTW * (threadIdx.x >> 6);
+    float4v acc[BM / 16][NTW];
+    MainloopPre<WT, NW, BM, NTW> pre;
+    mainloop_preload(pre, args, m0, ntile0);
+    gemm_mainloop<WT, NW, BM, NTW, TRANS>(args, m0, ntile0, smem, acc, pre);
+    float t = 0.f;
+#pragma unroll
+    for (int rt = 0; rt < BM / 16; rt++)
+#pragma unroll
+        for (int j = 0; j < NTW; j++) t += acc[rt][j][0] + acc[rt][j][3];
+    if (t == 1234.5678f) args.X[threadIdx.x] = t;
+}
+
+template <bool TRANS>
+static void run_probe(const char *name, GemmArgs a, int M, int iters) {
+    const int nnt = a.N / (12 * 2 * 16);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto launch = [&] { hipLaunchKernelGGL((mainloop_probe<W_Q4_0, 12, 128, 2, TRANS>), dim3(M / 128 * nnt), dim3(768), 0, 0, a, nnt); };
+    for (int i = 0; i < 3; i++) launch();
+    CK(hipGetLastError());
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; i++) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1000.0 / iters, fl = 2.0 * M * (double)a.N * a.K;
+    printf("%-34s M=%d N=%d K=%d  %8.1f us  %6.1f TF/s (2MNK)\n", name, M, a.N, a.K, us, fl / us * 1e-6);
+    fflush(stdout);
+}
+
 template <int WT, int EPI, int BN, int NW, int BM>
 static void run(const char *name, GemmArgs a, int M, int iters) {
     const int mt = M / BM, nt = a.N / BN;
@@ -122,6 +162,10 @@ int main(int argc, char **argv) {
         run<W_Q4_0, EPI_NONE, 384, 12, 128>("o    NONE <384,12,128>", o, M, iters);
         run<W_Q4_0, EPI_LN, 384, 12, 128>("down LN   <384,12,128>", d, M, iters);
         run<W_Q4_0, EPI_NONE, 384, 12, 128>("down NONE <384,12,128>", d, M, iters);
+    }
+    if (!strcmp(which, "trans")) {
+        run_probe<false>("qkv mainloop plain <12,128,2>", q, M, iters);
+        run_probe<true>("qkv mainloop trans <12,128,2>", q, M, iters);
     }
     if (!strcmp(which, "upnone")) run<W_Q4_0, EPI_NONE, 384, 12, 128>("up   NONE <384,12,128>", u, M, iters);
     if (!strcmp(which, "gelu")) {
