@@ -228,12 +228,21 @@ def main():
     # on the launch stream, in a separate pass of profile-steps steps right after
     # the timed region (the timed region itself carries no events)
     log(f"timed: {value:.1f} emb/s; per-kernel event pass")
+    # one row group in this pass (the timed steps run two on two streams,
+    # DESIGN.md §3): every profiled launch covers the whole batch alone, so its
+    # duration is the kernel's own and the roofline below is per launch
+    split_env = os.environ.get("BERT_AMD_SPLIT")
+    os.environ["BERT_AMD_SPLIT"] = "0"
     model.profile(True)
     for _ in range(args.profile_steps):
         step()
     torch.cuda.synchronize(dev)
     prof = model.profile_read()
     model.profile(False)
+    if split_env is None:
+        del os.environ["BERT_AMD_SPLIT"]
+    else:
+        os.environ["BERT_AMD_SPLIT"] = split_env
     kern = {}
     for name, (ms, cnt) in prof.items():
         fl = kernel_flops(name, B, N, hp)
@@ -390,8 +399,9 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "embeddings/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
-            "dtype_note": ("Q4 weights as exact fp16 (d_w*q split hi/lo) x Q8 integer activations on fp16 MFMA, "
-                           "f32 accumulate, per-block fold with d_a (ggml vec_dot_q4_x_q8_x)" if args.ftype.startswith("q")
+            "dtype_note": ("Q4 x Q8 (ggml vec_dot_q4_x_q8_x): FFN-up (and FFN-down at E=384) on int8 MFMA, exact "
+                           "block isum, per-block d_w*d_a fold in f32; QKV / O with Q4 weights as exact fp16 hi/lo "
+                           "pairs x Q8 integers on fp16 MFMA, per-block d_a fold" if args.ftype.startswith("q")
                            else f"{args.ftype} GEMM on {'fp16' if args.ftype == 'f16' else 'f32'} MFMA, f32 accumulate")
                           + "; attention split-fp16 MFMA (f32-level); LN/softmax sums f64",
             "data": "synthetic (deterministic splitmix64 token ids and weights; no checkpoints offline)",
@@ -402,6 +412,8 @@ def main():
             "roofline": roofline,
             "pipeline_mfma_frac": round(path_frac, 4),
             "kernels": kern,
+            "kernels_note": "per-kernel HIP-event pass with one row group (BERT_AMD_SPLIT=0); the timed steps "
+                            "run two row groups on two streams (runtime.cpp run_pipeline)",
             "cosine_vs_oracle": parity,
             "host_api": host_api,
             "ragged": ragged,

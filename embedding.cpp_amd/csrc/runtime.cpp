@@ -727,14 +727,17 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     const EmbedArgs ea = embed_args(ctx, R, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(wt, ea, (int)Mpad, st));
 
-    // Row groups (opt-in, env BERT_AMD_SPLIT=1): with the fused QKV + attention
-    // path the batch is split at a 128-row-aligned sentence boundary near M / 2
-    // and the two halves run their layers on two streams, so one half's
-    // HBM-bound LayerNorm GEMMs can overlap the other half's MFMA / VALU-bound
-    // kernels.  Groups own disjoint rows of every buffer; sentences never span
-    // groups, so results are identical.  Measured +0.9 % on the north-star
-    // batch, within run-to-run noise, and it halves every
-    // launch, so it is off by default (per-kernel profiles stay full-batch).
+    // Row groups (default; env BERT_AMD_SPLIT=0 turns them off, read per batch):
+    // with the fused QKV + attention path the batch is split at a 128-row-aligned
+    // sentence boundary near M / 2 and the two halves run their layers on two
+    // streams, so one half's LayerNorm GEMMs and VALU-bound FFN-up can overlap
+    // the other half's MFMA-heavy fused kernel, and batches too small to fill
+    // the GPU with one kernel at a time fill it with two.  Groups own disjoint
+    // rows of every buffer; sentences never span groups, so results are
+    // identical.  Measured (tools/ab_bench.sh, round 2): 1024 x 128 +1.9 %,
+    // 8..128-token batch +4.6 %, 8..40-token batch +20 %.  Per-kernel profiles
+    // (bench.py's event pass, tools/profile_round.sh) run with BERT_AMD_SPLIT=0
+    // so that every launch is the whole batch.
     struct Group {
         int64_t row0, rows;  // rows: 128-multiple
         int seq0, nseq;
@@ -742,7 +745,8 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     };
     Group G[2] = {{0, Mpad, 0, n_seqs, st}, {0, 0, 0, 0, nullptr}};
     int ng = 1;
-    static const bool split = std::getenv("BERT_AMD_SPLIT") != nullptr;
+    const char *split_env = std::getenv("BERT_AMD_SPLIT");
+    const bool split = !(split_env && split_env[0] == '0');
     if (split && fused_qkv_attn && ln_fused && n_seqs >= 512 && R.stream2) {
         int best = -1;
         for (int s = 1; s < n_seqs; s++)

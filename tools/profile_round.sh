@@ -19,6 +19,9 @@ step() {  # name seconds cmd...
 }
 B="$PWD/bench.py"
 step bench 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 256
+# kernel stats and counters per whole-batch launch (one row group; bench.py's own
+# event pass does the same), so rocprofv3 averages match the bench's roofline
+export BERT_AMD_SPLIT=0
 step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o $TAG -- python3 "$B" --steps 10 --warmup 3 --cpu-sample 0
 step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0
 step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0
@@ -28,6 +31,7 @@ python3 tools/hbm_summary.py "$OUT/fetch" "$OUT/write" "$TAG bench (C3 minilm q4
 python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" "minilm q4_0 batch=1024 seq_len=128" "$OUT/pmc_traffic.json" \
     "$TAG, tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py"
 cp "$(find "$OUT/stats" -name '*kernel_stats.csv' | head -1)" "$OUT/${TAG}_kernel_stats.csv"
+unset BERT_AMD_SPLIT
 step bench_pmc 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 256 --pmc-csv "$F,$W"
 tail -1 "$OUT/bench_pmc.log" > "$OUT/${TAG}_bench.json"
 cat "$OUT/${TAG}_bench.json"
