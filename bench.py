@@ -131,8 +131,8 @@ def pmc_traffic(csv_path: str, kernel_substr: str):
 
 # name fragments of the dominant kernels' mangled symbols (for PMC CSV lookup)
 KERNEL_SYMBOL = {
-    "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "gemm_kernel<2, 1,",
-    "gemm_down_ln": "gemm_kernel<2, 2,", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
+    "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "i8_up_gelu_kernel",
+    "gemm_down_ln": "i8_ln384_kernel", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
     "pool_l2": "pool_l2_kernel",
 }
 

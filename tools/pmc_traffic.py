@@ -14,8 +14,9 @@ from hbm_summary import load  # noqa: E402
 NAMES = {
     "qkv_attention": ["qkv_attention_kernel"],
     "gemm_up_gelu": ["i8_up_gelu_kernel", "q4r_up_gelu_kernel", "gemm_kernelILi2ELi1", "gemm_kernel<2, 1,"],
+    # default C3 build: o-proj on the split-fp16 LN GEMM, down on the int8 one
     "gemm_o_ln": ["gemm_kernelILi2ELi2", "gemm_kernel<2, 2,", "i8_ln384_kernel"],
-    "gemm_down_ln": ["gemm_kernelILi2ELi2", "gemm_kernel<2, 2,", "i8_ln384_kernel"],
+    "gemm_down_ln": ["i8_ln384_kernel", "gemm_kernelILi2ELi2", "gemm_kernel<2, 2,"],
     "embed_ln": ["embed_ln_kernel"],
     "pool_l2": ["pool_l2_kernel"],
 }
@@ -25,14 +26,18 @@ def main():
     fetch, write = load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE")
     out = {"workload": sys.argv[3], "source": sys.argv[5] if len(sys.argv) > 5 else "", "bytes_per_launch": {},
            "fetch_bytes": {}, "write_bytes": {},
-           "note": "FETCH_SIZE x2 + WRITE_SIZE, KB -> bytes, per dispatch; gemm_o_ln and gemm_down_ln share "
-                   "one kernel instantiation and are averaged together"}
+           "note": "FETCH_SIZE x2 + WRITE_SIZE, KB -> bytes, per dispatch; each name takes the kernels of "
+                   "its first symbol fragment that occurs (o-proj: split-fp16 LN GEMM, down: int8 LN GEMM)"}
     for name, frags in NAMES.items():
         fv, wv = [], []
-        for k in set(fetch) | set(write):
-            if any(f in k for f in frags):
-                fv += list(fetch.get(k, {}).values())
-                wv += list(write.get(k, {}).values())
+        keys = set(fetch) | set(write)
+        for f in frags:
+            hit = [k for k in keys if f in k]
+            if hit:
+                for k in hit:
+                    fv += list(fetch.get(k, {}).values())
+                    wv += list(write.get(k, {}).values())
+                break
         if fv and wv:
             fb = 2.0 * sum(fv) / len(fv) * 1024.0
             wb = sum(wv) / len(wv) * 1024.0
