@@ -575,277 +575,6 @@ __global__ __launch_bounds__(512) void i8_resid_kernel(GemmArgs g, int n_mtiles,
 }
 
 // ---------------------------------------------------------------------------
-// Ring-pipelined Q4_0 GEMM ("q4r"): the activation panel streams through a
-// 3-deep LDS ring filled by LDS-DMA (global_load_lds, full 128-byte row
-// lines, XOR-swizzled through the source address), the weight fragments go
-// global -> VGPR one chunk ahead, and every wait is a counted vmcnt on loads
-// issued by inline asm (the compiler sees none of them, so it never drains the
-// queue).  Workgroup tile: 128 tokens x 32 NWV features, wave w owns f-tile w
-// (32 features) x all four 32-token t-tiles; K in chunks of 128 (4 quant
-// blocks).  The per-block fold is ggml's (isum exact on the int8 MFMA,
-// dd = d_w * d_a exact on an f16 MFMA: here d_w one-hot x the row's four d_a,
-// so the one-hot is built once per block and f-tile, not per t-tile).
-namespace q4r {
-constexpr int BM = 128, T = 4, KC = 128, NBUF = 3;
-constexpr int AQ = BM * KC;     // int8 q of one chunk: 128 rows x 128 B (16 KiB)
-constexpr int AD = BM * 4 * 2;  // fp16 d_a of the chunk's 4 blocks, [piece q][64 lanes] dwords (1 KiB)
-constexpr int ABUF = AQ + AD;
-constexpr int APIECES = AQ / 1024;  // 1-KiB LDS-DMA pieces (8 rows x 128 B) per chunk
-constexpr int DPIECES = AD / 256;   // 256-B pieces (64 lanes x 4 B) per chunk
-}  // namespace q4r
-
-// row r's 16-B slot s lives at slot position s ^ swz(r): conflict-free
-// ds_read_b128 of the MFMA fragments (rows r, r + 1 differ in bank half)
-__device__ __forceinline__ int q4r_swz(int r) { return (r >> 1) & 7; }
-
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
-}
-// LDS-DMA: each lane's 16 (4) bytes from gsrc land at lds_dst + 16 (4) * lane
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
-__device__ __forceinline__ void glds4(const void *gsrc, uint32_t lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-// One stream position: chunk c of the tile whose first token row is m0 and
-// whose wave f-tile is ft.
-struct Q4RPos {
-    int64_t m0;
-    int ft, c;
-    bool ok;
-};
-
-template <int NWV>
-struct Q4RStream {
-    // weight fragments / scales of the next position, loaded by asm: the
-    // destinations are handed to the compiler only through q4r_wait_w
-    int4v w[4];
-    uint2 ws;
-};
-
-// Issue position P's A chunk (its share of the 1-KiB pieces and the d_a
-// pieces) into ring buffer `buf` (LDS byte address).
-template <int NWV>
-__device__ __forceinline__ void q4r_glds(const GemmArgs &g, const Q4RPos &P, uint32_t buf, int wv, int lane) {
-    const int K = g.K;
-    for (int p = wv; p < q4r::APIECES; p += NWV) {
-        const int row = 8 * p + (lane >> 3), sp = lane & 7, s = sp ^ q4r_swz(row);
-        glds16((const int8_t *)g.A.q + (P.m0 + row) * K + q4r::KC * P.c + 16 * s, buf + 1024 * p);
-    }
-    // d_a: piece q = row half (q >> 1) x dword (q & 1) of the chunk's 4 fp16
-    for (int q = wv; q < q4r::DPIECES; q += NWV) {
-        const int row = 64 * (q >> 1) + lane;
-        glds4((const uint16_t *)g.A.d + (P.m0 + row) * (K >> 5) + 4 * P.c + 2 * (q & 1), buf + q4r::AQ + 256 * q);
-    }
-}
-
-template <int NWV>
-__device__ __forceinline__ void q4r_wload(const GemmArgs &g, const Q4RPos &P, Q4RStream<NWV> &st, int lane) {
-    const int nkb = g.K >> 5;
-#pragma unroll
-    for (int bb = 0; bb < 4; bb++) {
-        const int4v *p = (const int4v *)g.Wi.q + ((int64_t)P.ft * nkb + 4 * P.c + bb) * 64 + lane;
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(st.w[bb]) : "v"(p) : "memory");
-    }
-    const uint2 *pw = (const uint2 *)g.Wi.dh + ((int64_t)P.ft * (nkb >> 2) + P.c) * 32 + (lane & 31);
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(st.ws) : "v"(pw) : "memory");
-}
-
-// wait until at most N VMEM ops are outstanding; the weight registers are
-// named so that no use of them is scheduled before the wait
-template <int N, int NWV>
-__device__ __forceinline__ void q4r_wait_w(Q4RStream<NWV> &st) {
-    asm volatile("s_waitcnt vmcnt(%5)"
-                 : "+v"(st.w[0]), "+v"(st.w[1]), "+v"(st.w[2]), "+v"(st.w[3]), "+v"(st.ws)
-                 : "i"(N)
-                 : "memory");
-}
-
-// Compute one chunk (4 blocks) of the wave's 4 t-tiles from ring buffer
-// `abuf`, with the chunk's weight fragments w[4] and fp16 d_w vector ws.
-__device__ __forceinline__ void q4r_chunk(const char *abuf, const int4v (&w)[4], uint2 ws, float16v (&acc)[4], int lane) {
-    const int l32 = lane & 31, hh = lane >> 5;
-    const float16v zf = {};
-    // d_a of the 4 blocks for each t-tile's token (the B operand of dd): two dwords
-    int4v dav[4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int row = 32 * t + l32;
-        const uint32_t *dq = (const uint32_t *)(abuf + q4r::AQ) + 128 * (row >> 6) + (row & 63);
-        dav[t] = int4v{(int)dq[0], (int)dq[64], 0, 0};
-    }
-    // A fragments one block ahead of their MFMAs (LDS latency hidden behind
-    // the current block's MFMAs and fold)
-    auto lds_x = [&](int4v (&x)[4], int bb) {
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int row = 32 * t + l32, s = 2 * bb + hh;
-            x[t] = *(const int4v *)(abuf + row * q4r::KC + 16 * (s ^ q4r_swz(row)));
-        }
-    };
-    int4v xbuf[2][4];
-    lds_x(xbuf[0], 0);
-#pragma unroll
-    for (int bb = 0; bb < 4; bb++) {
-        const int4v (&xa)[4] = xbuf[bb & 1];
-        if (bb < 3) lds_x(xbuf[(bb + 1) & 1], bb + 1);
-        // d_w one-hot at k = bb (lanes 0-31; lanes 32-63 hold k = 8.. and stay zero)
-        const uint32_t wsel = (bb < 2 ? ws.x : ws.y) & ((bb & 1) ? 0xffff0000u : 0x0000ffffu);
-        int4v oh = int4v{0, 0, 0, 0};
-        oh[bb >> 1] = hh ? 0 : (int)wsel;
-        // isum lands biased: the int accumulator starts at the bits of 1.5 * 2^23,
-        // so as a float it reads 1.5 * 2^23 + isum exactly (|isum| < 2^22) and
-        // the fold is two packed VALU ops per pair of outputs:
-        //   f = bits - 1.5 * 2^23 (exact);  acc = fma(f, dd, acc)  (ggml: sumf += d * (float) isum)
-        const int16v cbias = int16v{0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000,
-                                    0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000,
-                                    0x4B400000, 0x4B400000, 0x4B400000, 0x4B400000};
-        const float2v mb = {-12582912.0f, -12582912.0f};
-        int16v is[2];
-        float16v dd[2];
-        is[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[bb], xa[0], cbias, 0, 0, 0);
-        dd[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, oh), __builtin_bit_cast(half8, dav[0]),
-                                                       zf, 0, 0, 0);
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            if (t + 1 < 4) {
-                is[(t + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(w[bb], xa[t + 1], cbias, 0, 0, 0);
-                dd[(t + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, oh),
-                                                                         __builtin_bit_cast(half8, dav[t + 1]), zf, 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 16; i += 2) {
-                // (element copies first: clang's __builtin_bit_cast of an ext-vector
-                // element reads element 0 whatever the index)
-                const int e0 = is[t & 1][i], e1 = is[t & 1][i + 1];
-                float2v f = {__int_as_float(e0), __int_as_float(e1)};
-                f = f + mb;
-                float2v a = {acc[t][i], acc[t][i + 1]};
-                const float2v d = {dd[t & 1][i], dd[t & 1][i + 1]};
-                a = __builtin_elementwise_fma(f, d, a);
-                asm volatile("" : "+v"(a));
-                acc[t][i] = a[0];
-                acc[t][i + 1] = a[1];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
-// this wave's LDS-DMA instructions per chunk (A pieces p = wv, wv + NWV, ..;
-// d pieces q = wv < DPIECES)
-template <int NWV>
-__device__ __forceinline__ int q4r_nglds(int wv) {
-    return (q4r::APIECES - wv + NWV - 1) / NWV + (wv < q4r::DPIECES ? 1 : 0);
-}
-template <int NWV>
-__device__ __forceinline__ void q4r_wait_n(Q4RStream<NWV> &st, int n) {  // n: wave-uniform, 0..3
-    if (n >= 3) q4r_wait_w<3, NWV>(st);
-    else if (n == 2) q4r_wait_w<2, NWV>(st);
-    else if (n == 1) q4r_wait_w<1, NWV>(st);
-    else q4r_wait_w<0, NWV>(st);
-}
-
-// FFN up + GELU (bert.cpp:965-971), Q4_0: U = gelu(b + W.h) in the down
-// GEMM's Q8_0 format.  Persistent, one NWV-wave workgroup per CU; LDS: the A
-// ring and ggml's fp16 GELU table (entries [0, 0x8000 + neg_n], kernels.h
-// GELU_FLAT_LDS).  Stream of positions P = (tile j of this workgroup, chunk c):
-//   top of P:  W(P) in registers, chunk P in ring slot P % 3 (all waves)
-//   issue W(P + 1), then the DMAs of chunk P + 2 into slot (P + 2) % 3
-//   compute chunk P
-//   wait vmcnt(DMAs of P + 2): W(P + 1) and chunk P + 1 (this wave's part) landed
-//   barrier: chunk P + 1 complete in LDS, slot P % 3 free for P + 3
-//   last chunk of a tile: epilogue (its stores retire behind the next chunk)
-template <int NWV>
-__global__ __launch_bounds__(NWV * 64) void q4r_up_gelu_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
-    constexpr int NT = NWV * 64;
-    constexpr int RING = q4r::NBUF * q4r::ABUF;
-    __shared__ __attribute__((aligned(16))) char smem[RING + GELU_FLAT_LDS * 2];
-    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint16_t *gtab = (uint16_t *)(smem + RING);
-    const int nwg = n_mtiles * n_ntiles, nch = g.K / q4r::KC;
-    if ((int)blockIdx.x >= nwg) return;
-    const uint32_t ring = lds_addr(smem);
-    auto pos = [&](int j, int c) {
-        while (c >= nch) {
-            c -= nch;
-            j++;
-        }
-        Q4RPos P;
-        const int tile = (int)blockIdx.x + j * (int)gridDim.x;
-        P.ok = tile < nwg;
-        const int lin = xcd_linear(P.ok ? tile : 0, nwg);
-        const int mt = lin / n_ntiles, nt = lin - mt * n_ntiles;
-        P.m0 = (int64_t)mt * q4r::BM;
-        P.ft = nt * NWV + wv;
-        P.c = c;
-        return P;
-    };
-    const int ng = q4r_nglds<NWV>(wv);
-    Q4RStream<NWV> st;
-    {
-        const Q4RPos P0 = pos(0, 0), P1 = pos(0, 1);
-        q4r_glds<NWV>(g, P0, ring, wv, lane);
-        q4r_wload<NWV>(g, P0, st, lane);
-        if (P1.ok) q4r_glds<NWV>(g, P1, ring + q4r::ABUF, wv, lane);
-        // the GELU table (plain loads / LDS stores, ordered by the barrier below)
-        const int nflat8 = (0x8000 + g.gelu.neg_n + 1 + 7) / 8;
-        for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)g.gelu.full)[i];
-        q4r_wait_n<NWV>(st, P1.ok ? ng : 0);
-        __syncthreads();
-    }
-    const float xlo = h2f((uint16_t)(0x8000 | g.gelu.neg_n));
-    int slot = 0;
-    for (int j = 0;; j++) {
-        const Q4RPos Pt = pos(j, 0);
-        if (!Pt.ok) break;
-        float16v acc[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) acc[t] = float16v{};
-        for (int c = 0; c < nch; c++) {
-            const Q4RPos P1 = pos(j, c + 1), P2 = pos(j, c + 2);
-            const int4v w[4] = {st.w[0], st.w[1], st.w[2], st.w[3]};
-            const uint2 ws = st.ws;
-            if (P1.ok) q4r_wload<NWV>(g, P1, st, lane);
-            const int s2 = slot + 2 >= q4r::NBUF ? slot + 2 - q4r::NBUF : slot + 2;
-            if (P2.ok) q4r_glds<NWV>(g, P2, ring + s2 * q4r::ABUF, wv, lane);
-            q4r_chunk(smem + slot * q4r::ABUF, w, ws, acc, lane);
-            q4r_wait_n<NWV>(st, P2.ok ? ng : 0);
-            __builtin_amdgcn_s_barrier();
-            slot = slot + 1 == q4r::NBUF ? 0 : slot + 1;
-        }
-        // y = gelu(b + W.x) -> Q8_0 (ggml: add(repeat(b), mul_mat), then gelu)
-        const int col = 32 * Pt.ft + 16 * hh;
-        float bias[16];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const float4v b4 = *(const float4v *)(g.bias + col + 4 * q);
-#pragma unroll
-            for (int jj = 0; jj < 4; jj++) bias[4 * q + jj] = b4[jj];
-        }
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            float y[16];
-#pragma unroll
-            for (int i = 0; i < 16; i++) y[i] = h2f(gtab[f2h(fmaxf(bias[i] + acc[t][i], xlo))]);
-            i8_store_q8_half<W_Q4_0>(g.out_act, g.N, Pt.m0 + 32 * t + l32, Pt.ft, hh, y);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 static int n_cus_i8() {
     static int n = [] {
         int dev = 0, c = 0;
@@ -866,23 +595,8 @@ bool i8_gemm_supported(int epi, int N, int K) {
     return false;
 }
 
-// the ring-pipelined Q4_0 FFN-up kernel (q4r_*): opt-in, env BERT_AMD_Q4R=1
-// (measured no faster than the chunk-staged kernel above)
-static bool q4r_enabled() {
-    static const bool on = [] {
-        const char *e = std::getenv("BERT_AMD_Q4R");
-        return e && *e == '1';
-    }();
-    return on;
-}
-
 template <int WT>
 static hipError_t i8_gemm_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
-    if (WT == W_Q4_0 && epi == EPI_GELU_ACT && q4r_enabled() && a.N % 256 == 0 && Mpad % q4r::BM == 0) {
-        const int mt = Mpad / q4r::BM, nt = a.N / 256;
-        hipLaunchKernelGGL((q4r_up_gelu_kernel<8>), dim3(persistent_grid(mt * nt)), dim3(512), 0, s, a, mt, nt);
-        return hipGetLastError();
-    }
     if (epi == EPI_GELU_ACT) {
         if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS) return hipErrorInvalidValue;
         constexpr int NWV = I8_UP_WAVES, F = I8_UP_F, T = I8_UP_T;
