@@ -325,13 +325,15 @@ def test_mixed_lengths_group_like_separate_batches(model_dir):
     assert np.array_equal(full[[1, 3, 5]], long_)
 
 
-def test_packed_head_dim_64_equal_alone(model_dir, monkeypatch):
-    """Packed fused tiles at head dim 64 (e5-base f16, packing forced): every
-    sentence equals itself evaluated alone, bitwise."""
-    p, m = get_model(model_dir, "e5-base", "f16")
+@pytest.mark.parametrize("shape,ftype,n_layer,vocab", [("e5-base", "f16", None, 250002), ("bge-large", "q4_1", 2, 30522)])
+def test_packed_head_dim_64_equal_alone(shape, ftype, n_layer, vocab, model_dir, monkeypatch):
+    """Packed fused tiles at head dim 64 (e5-base f16, bge-large Q4_1 with 2
+    layers; packing forced): every sentence equals itself evaluated alone,
+    bitwise."""
+    p, m = get_model(model_dir, shape, ftype, 0.05, n_layer)
     rng = np.random.default_rng(5)
     lens = [1, 3, 31, 32, 33, 64, 7, 90, 20, 128, 45, 12] * 4
-    toks = [[101] + rng.integers(1000, 250002, max(n - 2, 0)).tolist() + [102] if n >= 2 else [101] for n in lens]
+    toks = [[101] + rng.integers(1000, vocab, max(n - 2, 0)).tolist() + [102] if n >= 2 else [101] for n in lens]
     monkeypatch.setenv("BERT_AMD_PACK", "1")
     full = m.eval_batch(toks)
     monkeypatch.setenv("BERT_AMD_PACK", "0")
