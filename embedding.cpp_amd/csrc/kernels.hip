@@ -5,9 +5,10 @@
 // the ggml semantics restated in SURVEY.md Appendix A wherever they are cheap
 // to reproduce exactly (Q8 activation quantisation, fp16 GELU/exp tables,
 // double-accumulated LayerNorm and softmax sums, fp16 activation rounding);
-// the weight GEMMs run on fp16 MFMA; Q4 weights are expanded once at load
-// into exact fp16 hi/lo pairs of d_w * q (runtime.cpp repack), so the
-// kernels apply only the activation scale d_a per block.
+// the weight GEMMs here run on fp16 MFMA; Q4 weights for them are expanded
+// once at load into exact fp16 hi/lo pairs of d_w * q (runtime.cpp repack), so
+// the kernels apply only the activation scale d_a per block.
+// The Q4 FFN GEMMs that run on the int8 MFMA instead live in gemm_i8.hip.
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
 #include "kernels_common.h"

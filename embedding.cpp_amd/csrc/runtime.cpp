@@ -734,7 +734,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     // the other half's MFMA-heavy fused kernel, and batches too small to fill
     // the GPU with one kernel at a time fill it with two.  Groups own disjoint
     // rows of every buffer; sentences never span groups, so results are
-    // identical.  Measured (tools/ab_bench.sh, round 2): 1024 x 128 +1.9 %,
+    // identical.  Measured (tools/ab_bench.sh, round 2): 1024 x 128 -0.6..+1.9 %,
     // 8..128-token batch +4.6 %, 8..40-token batch +20 %.  Per-kernel profiles
     // (bench.py's event pass, tools/profile_round.sh) run with BERT_AMD_SPLIT=0
     // so that every launch is the whole batch.
