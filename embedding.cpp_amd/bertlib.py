@@ -214,10 +214,11 @@ class BertModel:
         ntok = (ctypes.c_int32 * n)(*[len(a) for a in arrs])
         out_p = (F_P * n)(*[e.ctypes.data_as(F_P) for e in emb])
 
+        keep = (arrs, emb)  # the pointer arrays address these buffers
+
         def run():
-            # the closure holds the token arrays and `emb`: the pointer arrays address them
             self.lib.bert_eval_batch(self.ctx, 1, n, tok_p, ntok, out_p)
-            return emb if arrs else emb
+            return keep[1]
 
         return run, emb
 
