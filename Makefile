@@ -80,3 +80,8 @@ ref_consumers: $(BUILD)/ref_server $(BUILD)/ref_main
 $(BUILD)/qkva_time: tools/qkva_time.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
+
+# FETCH_SIZE / WRITE_SIZE calibration per access width (tools/pmc_calib.hip)
+$(BUILD)/pmc_calib: tools/pmc_calib.hip
+	@mkdir -p $(BUILD)
+	$(HIPCC) -O3 --offload-arch=gfx950 $< -o $@
