@@ -495,7 +495,12 @@ __device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW> &p
     const int tid = threadIdx.x, nkb = args.K >> 5;
 #pragma unroll
     for (int it = 0; it < IT; it++) {
-        const int item = tid + it * NT;
+        // every A address in the main loop is rebuilt from an opaque piece index
+        // where it is used: hoisted, the per-lane 64-bit pointers stayed live
+        // across the fused kernel's attention phase and were spilled (its
+        // scratch 64 -> 20 bytes per lane)
+        int item = tid + it * NT;
+        asm volatile("" : "+v"(item));
         if (item < ITEMS) a_load<WT>(pre.ar[it], args.A, args.K, m0, 0, item);
     }
     if constexpr (WT != W_F32) {
@@ -530,7 +535,8 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     AReg<WT> ar[IT];
 #pragma unroll
     for (int it = 0; it < IT; it++) {
-        const int item = tid + it * NT;
+        int item = tid + it * NT;
+        asm volatile("" : "+v"(item));
         if (item < ITEMS) a_store<WT, BM>(pre.ar[it], smem, item, unscale);
     }
     // W fragments of the two blocks in flight: block b lives in wf[b & 1] and
@@ -550,7 +556,8 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
         if (more) {
 #pragma unroll
             for (int it = 0; it < IT; it++) {
-                const int item = tid + it * NT;
+                int item = tid + it * NT;
+                asm volatile("" : "+v"(item));
                 if (item < ITEMS) a_load<WT>(ar[it], args.A, K, m0, (kc + 1) * KC, item);
             }
         }
@@ -648,7 +655,8 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
         if (more) {
 #pragma unroll
             for (int it = 0; it < IT; it++) {
-                const int item = tid + it * NT;
+                int item = tid + it * NT;
+                asm volatile("" : "+v"(item));
                 if (item < ITEMS) a_store<WT, BM>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
@@ -1002,6 +1010,7 @@ template <int WT, int D, int NDT = D / 32>
 __device__ __forceinline__ void attn_store_ctx(const AttnArgs &a, float16v *o, float rs, int64_t row, bool valid,
                                                int h, int hh, int dt0 = 0) {
     const int E = a.E;
+    asm volatile("" : "+v"(row));  // context addresses built here, not hoisted (spills)
 #pragma unroll
     for (int dt = 0; dt < NDT; dt++) {
 #pragma unroll
