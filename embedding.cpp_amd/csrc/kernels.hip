@@ -1443,7 +1443,9 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                         attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph, dh);
                     }
                     sum += __shfl_xor(sum, 32);
-                    attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + qrow, qrel + r < len, head,
+                    int orow = qrow;
+                    asm volatile("" : "+v"(orow));
+                    attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, head,
                                              hh, dh);
                 }
             }
