@@ -72,7 +72,8 @@ __device__ __forceinline__ void i8_stage_load(I8Items<(4 * BM + NT - 1) / NT> &s
 #pragma unroll
     for (int it = 0; it < IT; it++) {
         // unconditional (surplus threads re-load item % (4 BM)): exact wait counts
-        const int item = (threadIdx.x + it * NT) % (4 * BM);
+        int item = (threadIdx.x + it * NT) % (4 * BM);
+        asm volatile("" : "+v"(item));  // addresses built here, not hoisted out of the loop (spills)
         {
             const int r = item >> 2, bb = item & 3;
             const int64_t row = m0 + r;
@@ -94,7 +95,8 @@ __device__ __forceinline__ void i8_stage_store(const I8Items<(4 * BM + NT - 1) /
     using C = I8Chunk<BM, WT == W_Q4_1>;
 #pragma unroll
     for (int it = 0; it < IT; it++) {
-        const int item = threadIdx.x + it * NT;
+        int item = threadIdx.x + it * NT;
+        asm volatile("" : "+v"(item));
         if (4 * BM % NT == 0 || item < 4 * BM) {
             const int r = item >> 2, bb = item & 3;
             int4v *q = (int4v *)(buf + r * I8_LDQ + 32 * bb);
