@@ -778,6 +778,22 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         for (int i = tid; i < args.gelu.n_pad / 8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)args.gelu.compact)[i];
     }
 
+    // LN (384 wide): the residual rows of the first 16-row slice are loaded
+    // before the main loop (their latency hides behind it; the later slices'
+    // loads overlap the previous slice's row phase).  Wider rows would spill.
+    constexpr int LN_TPT = EPI == EPI_LN ? 64 * (BN / 32) / NT : 1;
+    constexpr bool XPRE = EPI == EPI_LN && BN == 384;
+    [[maybe_unused]] float4v xv[2][LN_TPT][2];
+    if constexpr (XPRE) {
+        LnTask t0[LN_TPT];  // (row, column) of ln_tasks; its bias loads come after the main loop
+#pragma unroll
+        for (int k = 0; k < LN_TPT; k++) {
+            const int t = tid + k * NT;
+            t0[k].r = (t >> 2) / (BN / 32);
+            t0[k].c = 32 * ((t >> 2) % (BN / 32)) + 8 * (t & 3);
+        }
+        ln_xload<BN / 32, NT>(xv[0], t0, args.X, m0);
+    }
     float4v acc[RT][NTW];
     {
         MainloopPre<WT, NW, BM, NTW> pre;
@@ -863,11 +879,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         constexpr int NSB = (EPI == EPI_LN && 2 * SLICE_BYTES <= SMEM) ? 2 : 1;  // LN: stage + red double-buffered
         constexpr bool LN = EPI == EPI_LN;
         [[maybe_unused]] LnTask tk[LN ? TPT : 1];
-        [[maybe_unused]] float4v xv[2][LN ? TPT : 1][2];
         [[maybe_unused]] float4v gb[LN ? 1 : TPT][2];
         if constexpr (LN) {
             ln_tasks<NBLK, NT>(tk, tid, args.bias);
-            ln_xload<NBLK, NT>(xv[0], tk, args.X, m0);
+            if constexpr (!XPRE) ln_xload<NBLK, NT>(xv[0], tk, args.X, m0);
         } else {
 #pragma unroll
             for (int k = 0; k < TPT; k++) {
