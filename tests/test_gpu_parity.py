@@ -267,6 +267,12 @@ def test_error_paths_leave_output_untouched(model_dir):
     assert np.all(np.isnan(out))
     bad_id = [101, 40000, 102]
     assert np.all(np.isnan(m.eval_batch([bad_id])))
+    # empty batch: nothing to do (the reference's loop runs zero times); an empty
+    # sentence is rejected before any launch, and the context stays usable
+    assert m.eval_batch([]).shape == (0, m.n_embd)
+    assert np.all(np.isnan(m.eval_batch([[101, 2000, 102], []])))
+    ok = m.eval_batch([[101, 2000, 102]])
+    assert np.all(np.isfinite(ok)) and abs(float(np.linalg.norm(ok)) - 1.0) < 1e-5
 
 
 def test_encode_path_and_tokenizer(model_dir):
