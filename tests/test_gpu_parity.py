@@ -532,3 +532,23 @@ def test_eval_batch_2d_array_matches_lists(model_dir):
     p, m = get_model(model_dir, "minilm", "q4_0")
     toks = np.array([sentence(900 + i, 64, 30522) for i in range(9)], np.int32)
     assert np.array_equal(m.eval_batch(toks), m.eval_batch([list(t) for t in toks]))
+
+
+def test_eval_batch_strided_rows_match_contiguous(model_dir):
+    """bert_eval_batch copies ids from / embeddings into contiguous caller rows
+    directly and gathers / scatters through its pinned buffers otherwise
+    (runtime.cpp eval_host_slice): strided caller rows give the same result."""
+    import ctypes
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    n, L, E = 7, 40, m.n_embd
+    toks = np.array([sentence(950 + i, L, 30522) for i in range(n)], np.int32)
+    ref = m.eval_batch(toks)  # both sides contiguous
+    big_t = np.zeros((2 * n, L), np.int32)
+    big_t[::2] = toks
+    big_e = np.full((2 * n, E), np.nan, np.float32)
+    tok_p = (bertlib.I_P * n)(*[big_t[2 * i].ctypes.data_as(bertlib.I_P) for i in range(n)])
+    ntok = (ctypes.c_int32 * n)(*([L] * n))
+    out_p = (bertlib.F_P * n)(*[big_e[2 * i].ctypes.data_as(bertlib.F_P) for i in range(n)])
+    m.lib.bert_eval_batch(m.ctx, 1, n, tok_p, ntok, out_p)
+    assert np.array_equal(big_e[::2], ref)
+    assert np.all(np.isnan(big_e[1::2]))  # rows between the caller's rows untouched
