@@ -231,18 +231,14 @@ def main():
     # one row group in this pass (the timed steps run two on two streams,
     # DESIGN.md §3): every profiled launch covers the whole batch alone, so its
     # duration is the kernel's own and the roofline below is per launch
-    split_env = os.environ.get("BERT_AMD_SPLIT")
-    os.environ["BERT_AMD_SPLIT"] = "0"
+    model.set_option("split", 0)
     model.profile(True)
     for _ in range(args.profile_steps):
         step()
     torch.cuda.synchronize(dev)
     prof = model.profile_read()
     model.profile(False)
-    if split_env is None:
-        del os.environ["BERT_AMD_SPLIT"]
-    else:
-        os.environ["BERT_AMD_SPLIT"] = split_env
+    model.set_option("split", int(os.environ.get("BERT_AMD_SPLIT", "1")[:1] != "0"))
     kern = {}
     for name, (ms, cnt) in prof.items():
         fl = kernel_flops(name, B, N, hp)
@@ -412,7 +408,7 @@ def main():
             "roofline": roofline,
             "pipeline_mfma_frac": round(path_frac, 4),
             "kernels": kern,
-            "kernels_note": "per-kernel HIP-event pass with one row group (BERT_AMD_SPLIT=0); the timed steps "
+            "kernels_note": "per-kernel HIP-event pass with one row group (bert_amd_set_option split 0); the timed steps "
                             "run two row groups on two streams (runtime.cpp run_pipeline)",
             "cosine_vs_oracle": parity,
             "host_api": host_api,

@@ -95,6 +95,8 @@ def lib() -> ctypes.CDLL:
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.bert_amd_debug_embed.restype = ctypes.c_int32
     L.bert_amd_debug_embed.argtypes = [ctypes.c_void_p, I_P, I_P, ctypes.c_int32, F_P, ctypes.c_void_p, ctypes.c_void_p]
+    L.bert_amd_set_option.restype = ctypes.c_int32
+    L.bert_amd_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
     L.bert_amd_workspace_rows.restype = ctypes.c_int64
     L.bert_amd_workspace_rows.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     L.bert_amd_last_error.restype = ctypes.c_char_p
@@ -253,6 +255,11 @@ class BertModel:
         if rc != 0:
             raise RuntimeError(f"bert_amd_debug_embed failed ({rc}): {last_error()}")
         return X, q, d
+
+    def set_option(self, key: str, value: int) -> None:
+        """bert_amd_set_option: "split" (0/1), "pack" (-1/0/1); results are identical either way."""
+        if self.lib.bert_amd_set_option(self.ctx, key.encode(), int(value)) != 0:
+            raise ValueError(f"bert_amd_set_option({key}, {value}) failed: {last_error()}")
 
     def workspace_rows(self, slot: int = 0) -> int:
         return int(self.lib.bert_amd_workspace_rows(self.ctx, slot))

@@ -208,6 +208,11 @@ struct Replica {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;               // second row group (run_pipeline)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // recorded on the stream of the last eval that used the workspace; every
+    // eval makes its own stream wait on it first (ws_acquire), so a call on one
+    // stream (the library's, a caller's, the null stream) never rewrites
+    // buffers an earlier call on another stream is still reading
+    hipEvent_t ev_free = nullptr;
     void *word = nullptr, *pos = nullptr, *type = nullptr;
     float *ln_e_w = nullptr, *ln_e_b = nullptr;
     std::vector<DevLayer> L;
@@ -242,6 +247,11 @@ struct bert_ctx {
     std::vector<std::unique_ptr<Replica>> reps;
     // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
     bool i8_o = false, i8_up = false, i8_down = false;
+    // run_pipeline knobs, read from the environment once at load
+    // (BERT_AMD_SPLIT, BERT_AMD_PACK) and changed only by bert_amd_set_option:
+    // two row groups on two streams (default on); fused-tile packing
+    // -1 = when it pays (default), 0 = never, 1 = always
+    int split = 1, pack = -1;
     std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
 };
 
@@ -518,6 +528,18 @@ void drain_profile(Replica &R) {
     R.pending.clear();
 }
 
+// Workspace hand-over between evals (Replica::ev_free): an eval's first
+// device operation waits for the previous eval's last one, whatever streams
+// the two ran on; the eval records the event behind its own last operation.
+bool ws_acquire(Replica &R, hipStream_t st) {
+    HIP_OK(hipStreamWaitEvent(st, R.ev_free, 0));
+    return true;
+}
+bool ws_release(Replica &R, hipStream_t st) {
+    HIP_OK(hipEventRecord(R.ev_free, st));
+    return true;
+}
+
 #define LAUNCH_OK(name, expr) LAUNCH_ON(name, st, expr)
 #define LAUNCH_ON(name, stream, expr)                                                     \
     do {                                                                                  \
@@ -727,7 +749,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     const EmbedArgs ea = embed_args(ctx, R, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(wt, ea, (int)Mpad, st));
 
-    // Row groups (default; env BERT_AMD_SPLIT=0 turns them off, read per batch):
+    // Row groups (default; ctx->split = 0 turns them off):
     // with the fused QKV + attention path the batch is split at a 128-row-aligned
     // sentence boundary near M / 2 and the two halves run their layers on two
     // streams, so one half's LayerNorm GEMMs and VALU-bound FFN-up can overlap
@@ -736,8 +758,9 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     // rows of every buffer; sentences never span groups, so results are
     // identical.  Measured (tools/ab_bench.sh, round 2): 1024 x 128 -0.6..+1.9 %,
     // 8..128-token batch +4.6 %, 8..40-token batch +20 %.  Per-kernel profiles
-    // (bench.py's event pass, tools/profile_round.sh) run with BERT_AMD_SPLIT=0
-    // so that every launch is the whole batch.
+    // (bench.py's event pass, tools/profile_round.sh) run with the split off
+    // (bert_amd_set_option "split" 0, or BERT_AMD_SPLIT=0 at load) so that
+    // every launch is the whole batch.
     struct Group {
         int64_t row0, rows;  // rows: 128-multiple
         int seq0, nseq;
@@ -745,9 +768,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     };
     Group G[2] = {{0, Mpad, 0, n_seqs, st}, {0, 0, 0, 0, nullptr}};
     int ng = 1;
-    const char *split_env = std::getenv("BERT_AMD_SPLIT");
-    const bool split = !(split_env && split_env[0] == '0');
-    if (split && fused_qkv_attn && ln_fused && n_seqs >= 512 && R.stream2) {
+    if (ctx->split && fused_qkv_attn && ln_fused && n_seqs >= 512 && R.stream2) {
         int best = -1;
         for (int s = 1; s < n_seqs; s++)
             if (h_off[s] % GEMM_BM == 0 &&
@@ -771,9 +792,8 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         std::vector<int32_t> &ht = w.h_tiles;
         ht.assign((size_t)2 * n_seqs, 0);
         auto span = [&](int s) { return (h_off[s + 1] - h_off[s] + 31) & ~31; };
-        // env BERT_AMD_PACK (A/B and tests; read per batch): "0" never packs, "1" always
-        const char *pack_env = std::getenv("BERT_AMD_PACK");
-        const bool no_pack = pack_env && pack_env[0] == '0', force_pack = pack_env && pack_env[0] == '1';
+        // ctx->pack (A/B and tests): 0 never packs, 1 always, -1 when it pays
+        const bool no_pack = ctx->pack == 0, force_pack = ctx->pack == 1;
         for (int gi = 0; gi < ng; gi++) {
             int32_t *t = ht.data() + 2 * G[gi].seq0;
             for (int s = G[gi].seq0, e = G[gi].seq0 + G[gi].nseq; s < e;) {
@@ -897,6 +917,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
     HIP_OK(hipStreamCreateWithFlags(&R.stream2, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&R.ev_free, hipEventDisableTiming));
     auto &tr = R.weight_allocs;
     const std::vector<float> word = table_f32(hm.word), pos = table_f32(hm.pos), type = table_f32(hm.type);
     if (!upload(tr, &R.word, word.data(), word.size() * 4) || !upload(tr, &R.pos, pos.data(), pos.size() * 4) ||
@@ -975,7 +996,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
 void free_replica(Replica &R) {
     if (R.stream) {
         hipSetDevice(R.device);
-        hipStreamSynchronize(R.stream);
+        hipDeviceSynchronize();  // caller streams may still read the workspace
     }
     drain_profile(R);
     for (void *p : R.ws.allocs) hipFree(p);
@@ -989,6 +1010,7 @@ void free_replica(Replica &R) {
     }
     if (R.ev_fork) hipEventDestroy(R.ev_fork);
     if (R.ev_join) hipEventDestroy(R.ev_join);
+    if (R.ev_free) hipEventDestroy(R.ev_free);
     if (R.stream) hipStreamDestroy(R.stream);
 }
 
@@ -1131,6 +1153,8 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
         return nullptr;
     }
     i8_select(ctx.get());
+    if (const char *e = std::getenv("BERT_AMD_SPLIT")) ctx->split = e[0] != '0';
+    if (const char *e = std::getenv("BERT_AMD_PACK")) ctx->pack = e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {
@@ -1209,10 +1233,11 @@ bool eval_host_slice(bert_ctx *ctx, Replica &R, bert_vocab_id **toks, const int3
         for (int s = s0; s < s1; s++) std::memcpy(w.h_tok + w.h_off[s - s0], toks[s], (size_t)ntok[s] * 4);
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
     const hipStream_t st = R.stream;
-    if (!ensure_workspace(ctx, R, Mpad, n, st)) return false;
+    if (!ensure_workspace(ctx, R, Mpad, n, st) || !ws_acquire(R, st)) return false;
     HIP_OK(hipMemcpyAsync(w.tok, tok_direct ? toks[s0] : w.h_tok, (size_t)M * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(w.off, w.h_off, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
-    if (!run_pipeline(ctx, R, w.tok, w.off, w.h_off, n, w.out, st)) return false;
+    const bool ok = run_pipeline(ctx, R, w.tok, w.off, w.h_off, n, w.out, st);
+    if (!ws_release(R, st) || !ok) return false;
     const int E = ctx->hp.n_embd;
     // caller rows contiguous (one [n][E] array, the usual case): the embeddings
     // go straight from the device into them, without the pinned bounce buffer
@@ -1548,6 +1573,13 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
     // the caller's stream, as given: NULL is HIP's null (legacy default)
     // stream, which is ordered with the caller's other work on it
     const hipStream_t st = (hipStream_t)hip_stream;
+    if (!ws_acquire(R, st)) return -3;
+    // every return below the acquire records the hand-over event first
+    struct Release {
+        Replica &R;
+        hipStream_t st;
+        ~Release() { ws_release(R, st); }
+    } release{R, st};
     try {
         // Short sentences in the caller's order may leave fused-kernel tiles
         // half empty: when the tile order (tile_order) needs fewer workgroups,
@@ -1654,7 +1686,7 @@ int32_t bert_amd_debug_embed(bert_ctx *ctx, const int32_t *tokens, const int32_t
         HIP_OK_RC(hipSetDevice(R.device), -3);
         const hipStream_t st = R.stream;
         const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
-        if (!ensure_workspace(ctx, R, Mpad, n_seqs, st)) return -3;
+        if (!ensure_workspace(ctx, R, Mpad, n_seqs, st) || !ws_acquire(R, st)) return -3;
         Workspace &w = R.ws;
         HIP_OK_RC(hipMemcpyAsync(w.tok, tokens, (size_t)M * 4, hipMemcpyHostToDevice, st), -3);
         HIP_OK_RC(hipMemcpyAsync(w.off, offsets, (size_t)(n_seqs + 1) * 4, hipMemcpyHostToDevice, st), -3);
@@ -1666,10 +1698,33 @@ int32_t bert_amd_debug_embed(bert_ctx *ctx, const int32_t *tokens, const int32_t
         if (d_out && act_scale_bytes(ctx->wtype))
             HIP_OK_RC(hipMemcpyAsync(d_out, w.Xa.d, (size_t)(M * (E / 32)) * act_scale_bytes(ctx->wtype),
                                      hipMemcpyDeviceToHost, st), -3);
+        ws_release(R, st);
         HIP_OK_RC(hipStreamSynchronize(st), -3);
     } catch (const std::exception &e) {
         set_err("%s", e.what());
         return -5;
+    }
+    return 0;
+}
+
+int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
+    if (!ctx || !key) {
+        set_err("bert_amd_set_option: invalid arguments");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const std::string k = key;
+    if (k == "split") {
+        ctx->split = value != 0;
+    } else if (k == "pack") {
+        if (value < -1 || value > 1) {
+            set_err("bert_amd_set_option: pack must be -1, 0 or 1");
+            return -2;
+        }
+        ctx->pack = value;
+    } else {
+        set_err("bert_amd_set_option: unknown option '%s'", key);
+        return -2;
     }
     return 0;
 }

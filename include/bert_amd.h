@@ -87,6 +87,14 @@ BERT_API int32_t bert_amd_debug_embed(struct bert_ctx *ctx, const int32_t *token
    that bert_encode_batch's n_batch_size bounds the working set. */
 BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
 
+/* Per-context pipeline options (read from the environment once at load,
+   BERT_AMD_SPLIT / BERT_AMD_PACK; this call changes them afterwards):
+     "split" 0 | 1     run large fused batches as two row groups on two streams
+     "pack"  -1 | 0 | 1 pack short sentences into shared fused-kernel tiles
+                        when it pays (-1, default) / never / always
+   Results are identical under every setting. */
+BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int32_t value);
+
 BERT_API const char *bert_amd_last_error(void);
 
 #ifdef __cplusplus

@@ -237,6 +237,44 @@ def test_device_resident_api_matches_host_api(model_dir):
     m.close()
 
 
+def test_eval_device_then_eval_batch_unsynchronised(model_dir):
+    """The workspace hand-over between evals on different streams (runtime.cpp
+    ws_acquire / ws_release): bert_amd_eval_device enqueued on the
+    null stream and on a caller stream, each immediately followed — no sync —
+    by bert_eval_batch (the library's own non-blocking stream) on a different
+    batch of a different size.  Both results equal the ones computed alone,
+    bitwise; without the hand-over event the second call rewrites the token,
+    offset and activation buffers the first is still reading."""
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    hip = Hip()
+    a = [sentence(900 + i, 128, 30522) for i in range(512)]
+    b = [sentence(1900 + i, n, 30522) for i, n in enumerate([77, 128, 5, 300, 64] * 20)]
+    want_a, want_b = m.eval_batch(a), m.eval_batch(b)
+    offs = np.zeros(len(a) + 1, np.int32)
+    offs[1:] = np.cumsum([len(t) for t in a])
+    ids = np.concatenate(a).astype(np.int32)
+    d_tok, d_off = hip.malloc(ids.nbytes), hip.malloc(offs.nbytes)
+    d_out = hip.malloc(len(a) * m.n_embd * 4)
+    st = hip.stream()
+    try:
+        hip.h2d(d_tok, ids)
+        hip.h2d(d_off, offs)
+        hip.sync(0)
+        for stream in (0, st):
+            for _ in range(3):
+                m.eval_device(d_tok, d_off, offs, len(a), d_out, stream)
+                got_b = m.eval_batch(b)  # its own stream; synchronises only itself
+                hip.sync(stream)
+                got_a = np.empty((len(a), m.n_embd), np.float32)
+                hip.d2h(got_a, d_out)
+                assert np.array_equal(got_b, want_b)
+                assert np.array_equal(got_a, want_a)
+    finally:
+        hip.destroy(st)
+        for q in (d_tok, d_off, d_out):
+            hip.free(q)
+
+
 def test_two_replicas_shard_like_one(model_dir):
     """bert_amd_load with devices [0, 0]: two replicas, two host threads, the
     batch split by token count — results identical to one replica."""
@@ -340,10 +378,13 @@ def test_packed_head_dim_64_equal_alone(shape, ftype, n_layer, vocab, model_dir,
     rng = np.random.default_rng(5)
     lens = [1, 3, 31, 32, 33, 64, 7, 90, 20, 128, 45, 12] * 4
     toks = [[101] + rng.integers(1000, vocab, max(n - 2, 0)).tolist() + [102] if n >= 2 else [101] for n in lens]
-    monkeypatch.setenv("BERT_AMD_PACK", "1")
-    full = m.eval_batch(toks)
-    monkeypatch.setenv("BERT_AMD_PACK", "0")
-    bad = [i for i in range(len(toks)) if not np.array_equal(full[i], m.eval(toks[i]))]
+    try:
+        m.set_option("pack", 1)
+        full = m.eval_batch(toks)
+        m.set_option("pack", 0)
+        bad = [i for i in range(len(toks)) if not np.array_equal(full[i], m.eval(toks[i]))]
+    finally:
+        m.set_option("pack", -1)
     assert not bad, [(i, lens[i]) for i in bad]
 
 
@@ -362,11 +403,13 @@ def test_packed_short_sentences_equal_alone(ftype, pack, model_dir, monkeypatch)
     rng = np.random.default_rng(31)
     lens = [1, 2, 3, 31, 32, 33, 5, 64, 64, 96, 32, 17, 9, 40, 100, 28] + rng.integers(1, 70, 584).tolist()
     toks = [[101] + rng.integers(1000, 30522, max(n - 2, 0)).tolist() + [102] if n >= 2 else [101] for n in lens]
-    if pack == "1":
-        monkeypatch.setenv("BERT_AMD_PACK", "1")
-    full = m.eval_batch(toks)
-    monkeypatch.setenv("BERT_AMD_PACK", "0")  # sentences alone: one per workgroup either way
-    alone = np.stack([m.eval(t) for t in toks])
+    try:
+        m.set_option("pack", 1 if pack == "1" else -1)
+        full = m.eval_batch(toks)
+        m.set_option("pack", 0)  # sentences alone: one per workgroup either way
+        alone = np.stack([m.eval(t) for t in toks])
+    finally:
+        m.set_option("pack", -1)
     bad = [i for i in range(len(toks)) if not np.array_equal(full[i], alone[i])]
     assert not bad, [(i, lens[i]) for i in bad]
     sub = list(range(16))
