@@ -453,11 +453,13 @@ static void act_convert(act_t *a, const float *x, int N, int K, uint32_t wtype) 
     a->K = K; a->vtype = wtype; a->f = (float *)x;
     if (wtype == T_F16) {
         a->h = (uint16_t *)malloc((size_t)N * K * 2);
+#pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < (int64_t)N * K; i++) a->h[i] = H16(x[i]);
     } else if (wtype == T_Q4_0 || wtype == T_Q4_1) {
         a->d = (float *)malloc((size_t)N * (K / QK) * 4);
         a->s = (float *)malloc((size_t)N * (K / QK) * 4);
         a->q = (int8_t *)malloc((size_t)N * K);
+#pragma omp parallel for schedule(static)
         for (int t = 0; t < N; t++)
             oracle_quantize_q8(x + (size_t)t * K, K, wtype == T_Q4_1, a->d + (size_t)t * (K / QK),
                                a->s + (size_t)t * (K / QK), a->q + (size_t)t * K);
@@ -465,25 +467,120 @@ static void act_convert(act_t *a, const float *x, int N, int K, uint32_t wtype) 
 }
 static void act_free(act_t *a) { free(a->h); free(a->d); free(a->s); free(a->q); memset(a, 0, sizeof *a); }
 
+/* The AVX2 checker (variant 0) over one weight row unpacked once (below):
+   identical operations to dot_f32 / dot_f16 / dot_q4_x_q8_x, without the
+   per-call variant test and the per-(row, token) re-decoding of the weight
+   blocks, so the compiler can vectorise the lane loops.  Variants 1 and 2
+   (ggml's other build orders, only used to measure the spread) keep the
+   per-call functions above. */
+static float dot_f32_rows(int n, const float *x, const float *y) { /* = dot_f32 variant 0 */
+    float acc[4][8] = {{0}};
+    int np = n & ~31;
+    for (int i = 0; i < np; i += 32)
+        for (int j = 0; j < 4; j++)
+            for (int l = 0; l < 8; l++) acc[j][l] = fmaf(x[i + 8 * j + l], y[i + 8 * j + l], acc[j][l]);
+    for (int l = 0; l < 8; l++) { acc[0][l] += acc[2][l]; acc[1][l] += acc[3][l]; }
+    for (int l = 0; l < 8; l++) acc[0][l] += acc[1][l];
+    float r4[4];
+    for (int l = 0; l < 4; l++) r4[l] = acc[0][l + 4] + acc[0][l];
+    return (r4[0] + r4[1]) + (r4[2] + r4[3]);
+}
+static float dot_f16_rows(int n, const float *x, const float *y) { /* = dot_f16 variant 0, inputs pre-widened */
+    int np = n & ~31;
+    double sumf = (double)dot_f32_rows(np, x, y);
+    for (int i = np; i < n; i++) sumf += (double)(x[i] * y[i]);
+    return (float)sumf;
+}
+/* = dot_q4_0_q8_0 / dot_q4_1_q8_1 variant 0; wq: the row's codes (q - 8 for
+   Q4_0, q for Q4_1), wd / wm: its fp16 d (and m) widened */
+static float dot_q4_rows(int n, const int8_t *wq, const float *wd, const float *wm, const float *ad, const float *as,
+                         const int8_t *aq) {
+    float acc[8] = {0};
+    float summs = 0.0f;
+    for (int b = 0; b < n / QK; b++) {
+        const float d = wd[b] * ad[b];
+        if (wm) summs += wm[b] * as[b];
+        const int8_t *w = wq + b * QK, *a = aq + b * QK;
+        for (int l = 0; l < 8; l++) {
+            const int s = w[4 * l] * a[4 * l] + w[4 * l + 1] * a[4 * l + 1] + w[4 * l + 2] * a[4 * l + 2] +
+                          w[4 * l + 3] * a[4 * l + 3];
+            acc[l] = fmaf(d, (float)s, acc[l]);
+        }
+    }
+    return wm ? hsum8(acc) + summs : hsum8(acc);
+}
+
 /* out[t][n] = bias[n] + (W . x_t)   — ggml_add(repeat(b), mul_mat(W, x)) */
 static void mul_mat_bias(const gtensor *W, const gtensor *bias, const act_t *a, int N, float *out) {
     const int K = (int)W->ne[0], NO = (int)W->ne[1];
     const size_t rb = row_bytes(W->type, K);
     const float *b = (const float *)bias->data;
+    const int fast = g_dot_variant == 0;
+    float *hx = NULL; /* F16 activations widened once (exact) for the fast path */
+    if (fast && W->type == T_F16) {
+        hx = (float *)malloc((size_t)N * K * 4);
 #pragma omp parallel for schedule(static)
-    for (int n = 0; n < NO; n++) {
-        const uint8_t *wr = W->data + (size_t)n * rb;
-        for (int t = 0; t < N; t++) {
-            float v;
-            switch (W->type) {
-                case T_F32: v = dot_f32(K, (const float *)wr, a->f + (size_t)t * K); break;
-                case T_F16: v = dot_f16(K, (const uint16_t *)wr, a->h + (size_t)t * K); break;
-                case T_Q4_0: v = dot_q4_0_q8_0(K, wr, a->d + (size_t)t * (K / QK), a->q + (size_t)t * K); break;
-                default: v = dot_q4_1_q8_1(K, wr, a->d + (size_t)t * (K / QK), a->s + (size_t)t * (K / QK), a->q + (size_t)t * K); break;
-            }
-            out[(size_t)t * NO + n] = b[n] + v;
-        }
+        for (int64_t i = 0; i < (int64_t)N * K; i++) hx[i] = F16(a->h[i]);
     }
+#pragma omp parallel
+    {
+        float *wf = (float *)malloc((size_t)K * 4), *wd = (float *)malloc((size_t)(K / QK + 1) * 4),
+              *wm = (float *)malloc((size_t)(K / QK + 1) * 4);
+        int8_t *wq = (int8_t *)malloc((size_t)K);
+#pragma omp for schedule(static)
+        for (int n = 0; n < NO; n++) {
+            const uint8_t *wr = W->data + (size_t)n * rb;
+            if (!fast) {
+                for (int t = 0; t < N; t++) {
+                    float v;
+                    switch (W->type) {
+                        case T_F32: v = dot_f32(K, (const float *)wr, a->f + (size_t)t * K); break;
+                        case T_F16: v = dot_f16(K, (const uint16_t *)wr, a->h + (size_t)t * K); break;
+                        case T_Q4_0: v = dot_q4_0_q8_0(K, wr, a->d + (size_t)t * (K / QK), a->q + (size_t)t * K); break;
+                        default:
+                            v = dot_q4_1_q8_1(K, wr, a->d + (size_t)t * (K / QK), a->s + (size_t)t * (K / QK),
+                                              a->q + (size_t)t * K);
+                            break;
+                    }
+                    out[(size_t)t * NO + n] = b[n] + v;
+                }
+                continue;
+            }
+            if (W->type == T_F16)
+                for (int k = 0; k < K; k++) wf[k] = F16(((const uint16_t *)wr)[k]);
+            if (W->type == T_Q4_0 || W->type == T_Q4_1) {
+                const int q1 = W->type == T_Q4_1, bs = q1 ? 20 : 18, off = q1 ? 4 : 2;
+                for (int bb = 0; bb < K / QK; bb++) {
+                    const uint8_t *blk = wr + (size_t)bb * bs;
+                    uint16_t dh, mh;
+                    memcpy(&dh, blk, 2);
+                    wd[bb] = F16(dh);
+                    if (q1) { memcpy(&mh, blk + 2, 2); wm[bb] = F16(mh); }
+                    for (int j = 0; j < 16; j++) {
+                        wq[bb * QK + j] = (int8_t)((blk[off + j] & 15) - (q1 ? 0 : 8));
+                        wq[bb * QK + j + 16] = (int8_t)((blk[off + j] >> 4) - (q1 ? 0 : 8));
+                    }
+                }
+            }
+            for (int t = 0; t < N; t++) {
+                float v;
+                switch (W->type) {
+                    case T_F32: v = dot_f32(K, (const float *)wr, a->f + (size_t)t * K); break;
+                    case T_F16: v = dot_f16_rows(K, wf, hx + (size_t)t * K); break;
+                    case T_Q4_0:
+                        v = dot_q4_rows(K, wq, wd, NULL, a->d + (size_t)t * (K / QK), NULL, a->q + (size_t)t * K);
+                        break;
+                    default:
+                        v = dot_q4_rows(K, wq, wd, wm, a->d + (size_t)t * (K / QK), a->s + (size_t)t * (K / QK),
+                                        a->q + (size_t)t * K);
+                        break;
+                }
+                out[(size_t)t * NO + n] = b[n] + v;
+            }
+        }
+        free(wf); free(wd); free(wm); free(wq);
+    }
+    free(hx);
 }
 
 /* ggml_norm then mul(repeat(w)) then add(repeat(b)), in place on x[N][E] */
@@ -593,6 +690,7 @@ int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
         act_convert(&a, x1, N, E, L->i_w->type);
         mul_mat_bias(L->i_w, L->i_b, &a, N, u);
         act_free(&a);
+#pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < (int64_t)N * I; i++) u[i] = F16(g_tab_gelu[H16(u[i])]);
         act_convert(&a, u, N, I, L->o2_w->type);
         mul_mat_bias(L->o2_w, L->o2_b, &a, N, tmp);
