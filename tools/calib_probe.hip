@@ -19,7 +19,7 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-constexpr int ITER = 256;
+constexpr int ITER = 4096;
 
 // op 0: v_fma_f32 x16 per iter; 1: v_cvt_f32_i32 + v_fma x16; 2: i8 mfma 32x32x32;
 // 3: f16 mfma 32x32x16; 4: scaled fp6 mfma 32x32x64; 5: i8 mfma + 16 cvt + 16 fma (fold);
@@ -27,7 +27,9 @@ constexpr int ITER = 256;
 // 8: two f16 mfma (int operands) + dd mfma + 16 fma
 template <int OP>
 __global__ void probe(float *out, long long *cyc, float seed) {
+    extern __shared__ char lds_pad[];  // 96 KiB dynamic: one workgroup per CU
     const int lane = threadIdx.x & 63;
+    if (seed < 0) lds_pad[threadIdx.x] = 0;
     float16v a0, a1, a2, a3;
     int16v i0, i1;
     for (int i = 0; i < 16; i++) {
@@ -49,7 +51,7 @@ __global__ void probe(float *out, long long *cyc, float seed) {
     }
     float16v dd = a3;
     __syncthreads();
-    const long long t0 = __builtin_amdgcn_s_memtime();
+    const long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < ITER; it++) {
         if constexpr (OP == 0) {
 #pragma unroll
@@ -60,6 +62,7 @@ __global__ void probe(float *out, long long *cyc, float seed) {
         } else if constexpr (OP == 1) {
 #pragma unroll
             for (int i = 0; i < 16; i++) {
+                asm volatile("" : "+v"(i0[i]));  // opaque: the cvt stays in the loop
                 float v = __builtin_fmaf((float)i0[i], a2[i], a0[i]);
                 asm volatile("" : "+v"(v));
                 a0[i] = v;
@@ -110,11 +113,14 @@ __global__ void probe(float *out, long long *cyc, float seed) {
             h0[0] += (_Float16)1;
         }
     }
-    const long long t1 = __builtin_amdgcn_s_memtime();
+    const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     float s = 0;
     for (int i = 0; i < 16; i++) s += a0[i] + a1[i] + (float)i0[i] + (float)i1[i];
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+    if (threadIdx.x == 0) {
+        cyc[2 * blockIdx.x] = t1 - t0;
+        cyc[2 * blockIdx.x + 1] = r1 - r0;
+    }
 }
 
 // VALU / MFMA instructions per iteration per wave, for the per-SIMD rate
@@ -135,27 +141,35 @@ static const OpInfo INFO[] = {{"v_fma_f32 x16", 16, 0},
 template <int OP>
 static void run(int waves_per_simd, float *d_out, long long *d_cyc) {
     const int threads = 256 * waves_per_simd, blocks = 256;
-    hipLaunchKernelGGL(probe<OP>, dim3(blocks), dim3(threads), 0, 0, d_out, d_cyc, 1e-3f);
+    const size_t lds = 96 * 1024;
+    CK(hipFuncSetAttribute((const void *)probe<OP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(probe<OP>, dim3(blocks), dim3(threads), lds, 0, d_out, d_cyc, 1e-3f);
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(probe<OP>, dim3(blocks), dim3(threads), 0, 0, d_out, d_cyc, 1e-3f);
+    hipLaunchKernelGGL(probe<OP>, dim3(blocks), dim3(threads), lds, 0, d_out, d_cyc, 1e-3f);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    std::vector<long long> c(blocks);
-    CK(hipMemcpy(c.data(), d_cyc, blocks * 8, hipMemcpyDeviceToHost));
-    double avg = 0;
-    for (long long v : c) avg += (double)v;
+    std::vector<long long> c(2 * blocks);
+    CK(hipMemcpy(c.data(), d_cyc, blocks * 16, hipMemcpyDeviceToHost));
+    double avg = 0, rt = 0;
+    for (int b = 0; b < blocks; b++) {
+        avg += (double)c[2 * b];
+        rt += (double)c[2 * b + 1];
+    }
     avg /= blocks;
+    rt /= blocks;  // 100 MHz ticks
+    const double ghz = avg / (rt * 10.0);  // memtime ticks per ns
     const OpInfo &I = INFO[OP];
     const double per_iter = avg / ITER;  // cycles per iteration of every wave on the SIMD
     const double per_wave_iter = per_iter / waves_per_simd;
-    printf("%-36s waves/SIMD %d: %7.1f cyc per wave-iteration (valu %d, mfma %d)  wall %.3f ms\n", I.name,
-           waves_per_simd, per_wave_iter, I.valu, I.mfma, ms);
+    const double ns_iter = rt * 10.0 / ITER / waves_per_simd;  // SIMD ns per wave-iteration
+    printf("%-36s w/SIMD %d: %6.2f ticks  %6.2f ns (= %5.1f cyc @2.4GHz) per wave-iter (valu %d mfma %d); tick %.2f GHz; wall %.3f ms\n",
+           I.name, waves_per_simd, per_wave_iter, ns_iter, ns_iter * 2.4, I.valu, I.mfma, ghz, ms);
     fflush(stdout);
 }
 
@@ -163,7 +177,7 @@ int main() {
     float *d_out;
     long long *d_cyc;
     CK(hipMalloc(&d_out, 256 * 1024 * 4));
-    CK(hipMalloc(&d_cyc, 256 * 8));
+    CK(hipMalloc(&d_cyc, 256 * 16));
     for (int w = 1; w <= 4; w *= 2) {
         run<0>(w, d_out, d_cyc);
         run<1>(w, d_out, d_cyc);
