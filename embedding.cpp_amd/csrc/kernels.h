@@ -25,10 +25,14 @@ namespace bertamd {
 // follows it exactly like ggml's vec_dot_type:
 //   W_F32 -> f32, W_F16 -> fp16 (RNE), W_Q4_0 -> Q8_0 (int8 + fp16 d),
 //   W_Q4_1 -> Q8_1 (int8 + f32 d)
-enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3 };
+// W_Q4_0D: Q4_0 weights whose GEMMs run on the block-scaled fp6 MFMA
+// (gemm_f6.hip); the same ggml Q8_0 activations (d, q), stored as Q8D: per
+// 32-block 48 bytes of fp6 digit codes (kernels_common.h q8d_*) + fp16 d.
+enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3, W_Q4_0D = 4 };
+constexpr int Q8D_BLK = 48;  // code bytes per Q8D block
 
 struct ActPtr {
-    void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K]
+    void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K] | Q8D codes [M][K/32][48 B]
     void *d = nullptr;  // per-32-block scale [M][K/32]: fp16 (Q8_0) | f32 (Q8_1)
 };
 
@@ -66,6 +70,20 @@ struct I8W {
     const uint16_t *dh = nullptr;
 };
 
+// Q4_0 weights for the fp6-MFMA GEMMs (gemm_f6.hip), repacked at load
+// (runtime.cpp upload_f6) per 32-row f-tile ft (features 32 ft .. 32 ft + 31,
+// natural order) and 32-wide k block b: the 32 codes of q - 8 (e2m3
+// sign-magnitude, 6 bits each, element k at Q8D position q8d_pos(k)) as
+//   q16: [N/32][K/32][32 rows] x 16 B (code dwords 0-3)
+//   q8 : [N/32][K/32][32 rows] x 8 B  (code dwords 4-5)
+//   dw : [N/32][K/128][32 rows] x 4 dwords: dword v = fp16 d_w of block 4 g + v
+//        in the low half (the d_w operand of the d_w * d_a MFMA)
+struct F6W {
+    const uint4 *q16 = nullptr;
+    const uint2 *q8 = nullptr;
+    const uint4 *dw = nullptr;
+};
+
 enum Epi : int {
     EPI_QKV = 0,       // y = b + W.x split hi/lo for attention (Q|K row-major, V transposed)
     EPI_GELU_ACT = 1,  // gelu(b + W.x) in the next matmul's activation format
@@ -98,6 +116,7 @@ struct GemmArgs {
     int K = 0;
     WPtr W;                // [N][K] repacked
     I8W Wi;                // the same weights for the int8 path (Q4 GEMMs in gemm_i8.hip)
+    F6W Wf;                // the same weights for the fp6 path (Q4_0 GEMMs in gemm_f6.hip)
     int N = 0;
     const float *bias = nullptr;   // [N]
     // EPI_QKV: y = b + W.x (f32, as ggml), stored split for the attention MFMAs:
@@ -178,5 +197,12 @@ bool gemm_gelu_blk8(int wtype);
 // EPI_LN (N == 384), EPI_RESID (N % 256 == 0); K % 128 == 0; Mpad % 128 == 0.
 bool i8_gemm_supported(int epi, int N, int K);
 hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
+
+// Q4_0 x Q8D GEMMs on the fp6 MFMA (gemm_f6.hip): A in Q8D, output in Q8D;
+// EPI_GELU_ACT (N % 512 == 0), EPI_LN (N == 384); K % 128 == 0; Mpad % 128 == 0.
+bool f6_gemm_supported(int epi, int N, int K);
+hipError_t launch_gemm_f6(int epi, const GemmArgs &a, int Mpad, hipStream_t s);
+// Q8_0 (int8 q [nblk][32]) <-> Q8D codes [nblk][48 B]; the fp16 d are shared
+hipError_t launch_q8_convert(bool to_q8d, const void *src, void *dst, int64_t nblk, hipStream_t s);
 
 }  // namespace bertamd

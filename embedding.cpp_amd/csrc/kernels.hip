@@ -1031,7 +1031,14 @@ __device__ __forceinline__ void attn_store_ctx(const AttnArgs &a, float16v *o, f
 #pragma unroll
         for (int j = 0; j < 16; j++) o[dt][j] *= rs;
         const int col0 = h * D + (dt0 + dt) * 32;
-        if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+        if constexpr (WT == W_Q4_0D) {
+            // the lane pair's 32 values are one Q8D block, in its position order
+            float y[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) y[j] = o[dt][j];
+            const int64_t bi = row * (E >> 5) + (col0 >> 5);
+            q8d_store_pair((char *)a.ctx.q + bi * Q8D_BLK, (uint16_t *)a.ctx.d + bi, hh, y, valid);
+        } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
             float amax = 0.f;
 #pragma unroll
             for (int j = 0; j < 16; j++) amax = fmaxf(amax, fabsf(o[dt][j]));
@@ -1770,6 +1777,7 @@ hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s) 
         case W_F16: return embed_t<W_F16>(a, Mpad, s);
         case W_Q4_0: return embed_t<W_Q4_0>(a, Mpad, s);
         case W_Q4_1: return embed_t<W_Q4_1>(a, Mpad, s);
+        case W_Q4_0D: return embed_t<W_Q4_0D>(a, Mpad, s);
     }
     return hipErrorInvalidValue;
 }
@@ -1893,6 +1901,7 @@ hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs
         case W_F16: return attn_w<W_F16>(d_head, a, n_seqs, max_len, s);
         case W_Q4_0: return attn_w<W_Q4_0>(d_head, a, n_seqs, max_len, s);
         case W_Q4_1: return attn_w<W_Q4_1>(d_head, a, n_seqs, max_len, s);
+        case W_Q4_0D: return attn_w<W_Q4_0D>(d_head, a, n_seqs, max_len, s);
     }
     return hipErrorInvalidValue;
 }
@@ -1916,6 +1925,7 @@ hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const
         case W_F16: return ln_w<W_F16>(X, Mpad, E, w, b, eps, out, s);
         case W_Q4_0: return ln_w<W_Q4_0>(X, Mpad, E, w, b, eps, out, s);
         case W_Q4_1: return ln_w<W_Q4_1>(X, Mpad, E, w, b, eps, out, s);
+        case W_Q4_0D: return ln_w<W_Q4_0D>(X, Mpad, E, w, b, eps, out, s);
     }
     return hipErrorInvalidValue;
 }
