@@ -259,12 +259,10 @@ __device__ __forceinline__ void f6_block(const char *buf, const F6Lane &ln, cons
         if constexpr (F6_ABL & 1) {
             acc[p / T][p % T][p] += is[p & 1][p] + dd[p & 1][p];
         } else {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                float v = __builtin_fmaf(is[p & 1][i], dd[p & 1][i], acc[p / T][p % T][i]);
-                asm volatile("" : "+v"(v));  // keep the fold here: sunk past the MFMAs it would keep every tile live
-                acc[p / T][p % T][i] = v;
-            }
+            // v_pk_fma_f32: two of the lane's 16 sums per issue
+            float16v v = __builtin_elementwise_fma(is[p & 1], dd[p & 1], acc[p / T][p % T]);
+            asm volatile("" : "+v"(v));  // keep the fold here: sunk past the MFMAs it would keep every tile live
+            acc[p / T][p % T] = v;
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -274,12 +272,14 @@ __device__ __forceinline__ void f6_block(const char *buf, const F6Lane &ln, cons
 // whole K for the wave's F f-tiles x T t-tiles (tt0 = 0: the wave covers the
 // BM rows); `pp` holds this tile's first loads on entry and the next tile's
 // (m0n, ft0n) on return.  Returns after a final barrier (the LDS may be reused).
-template <int NT, int BM, int F, int T, int WR, bool PIPE>
+// NCH = K / 128 chunks (a compile-time trip count; the loop stays rolled:
+// unrolled, the scheduler's hoisting spilled 36-604 B per lane).
+template <int NT, int BM, int F, int T, int WR, bool PIPE, int NCH>
 __device__ __forceinline__ void f6_mainloop(const GemmArgs &g, int64_t m0, int ft0, int64_t m0n, int ft0n, char *smem,
                                             F6Pipe<NT, BM, F, WR> &pp, float16v (&acc)[F][T]) {
     using C = F6Chunk<BM>;
     const int lane = threadIdx.x & 63, hh = lane >> 5;
-    const int nkb = g.K >> 5, nch = g.K / F6_KC;
+    const int nkb = 4 * NCH, nch = NCH;
     // this lane's token rows in the chunk buffer (t-tile 0), its plane half
     F6Lane ln{(lane & 31) * Q8D_BLK + 16 * hh, 32 - 8 * hh, 16 * (lane & 31)};
     asm volatile("" : "+v"(ln.lb), "+v"(ln.l8), "+v"(ln.lt));
@@ -295,6 +295,7 @@ __device__ __forceinline__ void f6_mainloop(const GemmArgs &g, int64_t m0, int f
     f6_stage_store<BM, NT>(pp.st, pp.mp, smem);
     wscale_use();
     __syncthreads();
+#pragma unroll 1
     for (int c = 0; c < nch; c++) {
         const bool more = c + 1 < nch;
         const int b0 = 4 * c;
@@ -347,7 +348,7 @@ __device__ __forceinline__ int f6_row(int i, int hh) { return 8 * (i >> 2) + 4 *
 // one 8-wave workgroup per CU walks 64 x 512 tiles; ggml's fp16 GELU table
 // (entries [0, 0x8000 + neg_n], kernels.h GELU_FLAT_LDS) is read into LDS once.
 // Wave w: f-tiles 2w, 2w + 1 of the tile, both 32-token t-tiles.
-template <int NWV, int F, int T>
+template <int NWV, int F, int T, int NCH>
 __global__ __launch_bounds__(NWV * 64) void f6_up_gelu_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
     constexpr int NT = NWV * 64, BM = 32 * T, BN = 32 * NWV * F;
     using C = F6Chunk<BM>;
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(NWV * 64) void f6_up_gelu_kernel(GemmArgs g, int n_
         int ft0n = ft0;
         if (tile + (int)gridDim.x < nwg) coords(tile + gridDim.x, m0n, ft0n);
         float16v acc[F][T];
-        f6_mainloop<NT, BM, F, T, F6_UP_WR, F6_UP_PIPE>(g, m0, ft0, m0n, ft0n, smem, pp, acc);
+        f6_mainloop<NT, BM, F, T, F6_UP_WR, F6_UP_PIPE, NCH>(g, m0, ft0, m0n, ft0n, smem, pp, acc);
         const int64_t mc = m0;
         const int fc = ft0;
         m0 = m0n;
@@ -423,6 +424,27 @@ __global__ __launch_bounds__(NWV * 64) void f6_up_gelu_kernel(GemmArgs g, int n_
 // both 32-token t-tiles, so a row's 384 values are spread over 12 waves x 2
 // lane halves x 16.  ggml_norm's double sums go lane -> lane pair -> the
 // twelve waves (LDS partials, fixed order).
+// Q8 block of 32 outputs held as 16 per lane by lanes l and l ^ 32 in the
+// natural-order accumulator layout (element 4q + j of lane half hh is column
+// 8q + 4hh + j), stored as ggml's Q8_0 (int8 codes + fp16 d; the i8 path's
+// i8_store_q8_half arithmetic): four dwords per lane.
+__device__ __forceinline__ void f6_store_q8_0(const ActPtr &out, int64_t row, int blk, int hh, const float (&y)[16]) {
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; i++) amax = fmaxf(amax, fabsf(y[i]));
+    {
+        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+    }
+    float d, id;
+    q8_scales(amax, d, id);
+    uint32_t *dst = (uint32_t *)((int8_t *)out.q + row * 384 + 32 * blk + 4 * hh);
+#pragma unroll
+    for (int q = 0; q < 4; q++) dst[2 * q] = q8_pack4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3], id);
+    if (hh == 0) ((uint16_t *)out.d)[row * 12 + blk] = f2h(d);
+}
+
+template <int NCH, bool OUT_Q8D>
 __global__ __launch_bounds__(768) void f6_ln384_kernel(GemmArgs g, int n_mtiles) {
     constexpr int NT = 768, BM = 64, F = 1, T = 2, NCOL = 384, NWV = 12, NBO = NCOL / 32;
     using C = F6Chunk<BM>;
@@ -443,7 +465,7 @@ __global__ __launch_bounds__(768) void f6_ln384_kernel(GemmArgs g, int n_mtiles)
         const int64_t m0 = m0n;
         if (tile + (int)gridDim.x < n_mtiles) m0n = (int64_t)f6_xcd_linear(tile + gridDim.x, n_mtiles) * BM;
         float16v acc[F][T];
-        f6_mainloop<NT, BM, F, T, F6_LN_WR, F6_LN_PIPE>(g, m0, ft0, m0n, ft0, smem, pp, acc);
+        f6_mainloop<NT, BM, F, T, F6_LN_WR, F6_LN_PIPE, NCH>(g, m0, ft0, m0n, ft0, smem, pp, acc);
         if constexpr ((F6_ABL & 32) != 0) {
             float cs = 0.f;
 #pragma unroll
@@ -521,7 +543,10 @@ __global__ __launch_bounds__(768) void f6_ln384_kernel(GemmArgs g, int n_mtiles)
                 *(float4v *)(xr + 8 * q) = float4v{y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]};
             }
             const int64_t bi = row * NBO + ft0;
-            q8d_store_pair((char *)g.out_act.q + bi * Q8D_BLK, (uint16_t *)g.out_act.d + bi, hh, y);
+            if constexpr (OUT_Q8D)
+                q8d_store_pair((char *)g.out_act.q + bi * Q8D_BLK, (uint16_t *)g.out_act.d + bi, hh, y);
+            else
+                f6_store_q8_0(g.out_act, row, ft0, hh, y);
         }
         // the next tile's main loop reuses `red` only after its own barriers
     }
@@ -591,23 +616,32 @@ static int f6_persistent_grid(int tiles) { return std::max(1, std::min(tiles, st
 constexpr int F6_UP_WAVES = 8, F6_UP_F = 2, F6_UP_T = 2;
 
 bool f6_gemm_supported(int epi, int N, int K) {
-    if (K % F6_KC) return false;
+    if (K != 384 && K != 1536) return false;  // the chunk loops are unrolled per K
     if (epi == EPI_GELU_ACT) return N % (32 * F6_UP_WAVES * F6_UP_F) == 0;
     if (epi == EPI_LN) return N == 384;
     return false;
 }
 
-hipError_t launch_gemm_f6(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
+hipError_t launch_gemm_f6(int epi, const GemmArgs &a, int Mpad, hipStream_t s, int out_type) {
     if (!f6_gemm_supported(epi, a.N, a.K) || Mpad % 128) return hipErrorInvalidValue;
+    if (out_type != W_Q4_0D && (epi != EPI_LN || out_type != W_Q4_0)) return hipErrorInvalidValue;
     if (epi == EPI_GELU_ACT) {
         if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS) return hipErrorInvalidValue;
         constexpr int NWV = F6_UP_WAVES, F = F6_UP_F, T = F6_UP_T;
         const int mt = Mpad / (32 * T), nt = a.N / (32 * NWV * F);
-        hipLaunchKernelGGL((f6_up_gelu_kernel<NWV, F, T>), dim3(f6_persistent_grid(mt * nt)), dim3(NWV * 64), 0, s, a,
-                           mt, nt);
+        if (a.K == 384)
+            hipLaunchKernelGGL((f6_up_gelu_kernel<NWV, F, T, 3>), dim3(f6_persistent_grid(mt * nt)), dim3(NWV * 64), 0,
+                               s, a, mt, nt);
+        else
+            hipLaunchKernelGGL((f6_up_gelu_kernel<NWV, F, T, 12>), dim3(f6_persistent_grid(mt * nt)), dim3(NWV * 64), 0,
+                               s, a, mt, nt);
     } else {
         const int mt = Mpad / 64;
-        hipLaunchKernelGGL(f6_ln384_kernel, dim3(f6_persistent_grid(mt)), dim3(768), 0, s, a, mt);
+        const dim3 grid(f6_persistent_grid(mt)), blk(768);
+        const bool q8d = out_type == W_Q4_0D;
+        auto kern = a.K == 384 ? (q8d ? f6_ln384_kernel<3, true> : f6_ln384_kernel<3, false>)
+                               : (q8d ? f6_ln384_kernel<12, true> : f6_ln384_kernel<12, false>);
+        hipLaunchKernelGGL(kern, grid, blk, 0, s, a, mt);
     }
     return hipGetLastError();
 }

@@ -176,7 +176,8 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles);
 bool qkv_attention_supported(int wtype, int E, int H, int max_len);
 // head pairs per GEMM main loop of that kernel (its QKV copy's tile grouping, runtime.cpp)
 int qkv_attention_ntw(int wtype);
-// n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
+// n_blocks: tiles (a.tiles) or sentences (a.tiles == null); wtype W_Q4_0D: Q4_0
+// weights, int8 Q8_0 input, context stored as Q8D
 hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s);
 // out_row (optional): output row of each sentence (default: its batch index)
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s,
@@ -198,10 +199,11 @@ bool gemm_gelu_blk8(int wtype);
 bool i8_gemm_supported(int epi, int N, int K);
 hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
 
-// Q4_0 x Q8D GEMMs on the fp6 MFMA (gemm_f6.hip): A in Q8D, output in Q8D;
-// EPI_GELU_ACT (N % 512 == 0), EPI_LN (N == 384); K % 128 == 0; Mpad % 128 == 0.
+// Q4_0 x Q8D GEMMs on the fp6 MFMA (gemm_f6.hip): A in Q8D; EPI_GELU_ACT
+// (N % 512 == 0, output Q8D), EPI_LN (N == 384, output `out_type` W_Q4_0D or
+// ggml's Q8_0 W_Q4_0); K 384 or 1536; Mpad % 128 == 0.
 bool f6_gemm_supported(int epi, int N, int K);
-hipError_t launch_gemm_f6(int epi, const GemmArgs &a, int Mpad, hipStream_t s);
+hipError_t launch_gemm_f6(int epi, const GemmArgs &a, int Mpad, hipStream_t s, int out_type = W_Q4_0D);
 // Q8_0 (int8 q [nblk][32]) <-> Q8D codes [nblk][48 B]; the fp16 d are shared
 hipError_t launch_q8_convert(bool to_q8d, const void *src, void *dst, int64_t nblk, hipStream_t s);
 

@@ -1240,7 +1240,9 @@ constexpr int QKVA_NW = 12;  // waves
 
 // D: head dim; NTW: 192-feature units per main loop (qkv_attention_ntw); PK:
 // sentence tiles (a.tiles)
-template <int WT, int D, int NTW, bool PK>
+// CT: the context's activation format (WT, or W_Q4_0D: Q4_0 weights read from
+// int8 Q8_0 activations, context stored as Q8D for the fp6 O projection)
+template <int WT, int D, int NTW, bool PK, int CT = WT>
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
     constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
     constexpr int NW = QKVA_NW, BM = 128, RT = BM / 16;
@@ -1467,7 +1469,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     sum += __shfl_xor(sum, 32);
                     int orow = qrow;
                     asm volatile("" : "+v"(orow));
-                    attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, head,
+                    attn_store_ctx<CT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, head,
                                              hh, dh);
                 }
             }
@@ -1476,28 +1478,28 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     }
 }
 
-template <int WT, int D>
+template <int WT, int D, int CT>
 static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
     const bool pk = a.tiles != nullptr;
     if (qkv_attention_ntw(WT) == 2) {
         if (pk)
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, true, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
         else
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, false, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
     } else {
         if (pk)
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, true, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
         else
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, false, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
     }
     return hipGetLastError();
 }
 
-template <int WT>
+template <int WT, int CT = WT>
 static hipError_t qkv_attn_w(const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
     switch (a.H > 0 ? a.E / a.H : 0) {
-        case 32: return qkv_attn_t<WT, 32>(g, a, n_blocks, s);
-        case 64: return qkv_attn_t<WT, 64>(g, a, n_blocks, s);
+        case 32: return qkv_attn_t<WT, 32, CT>(g, a, n_blocks, s);
+        case 64: return qkv_attn_t<WT, 64, CT>(g, a, n_blocks, s);
     }
     return hipErrorInvalidValue;
 }
@@ -1545,6 +1547,7 @@ hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a,
     switch (wtype) {
         case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, s);
         case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, s);
+        case W_Q4_0D: return qkv_attn_w<W_Q4_0, W_Q4_0D>(g, a, n_blocks, s);
         case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, s);
     }
     return hipErrorInvalidValue;

@@ -176,6 +176,7 @@ struct DevMat {
 struct DevLayer {
     WPtr qkv, o, up, down;
     I8W o8, up8, down8;  // Q4 weights for the int8-MFMA GEMMs (gemm_i8.hip)
+    F6W o6, up6, down6;  // Q4_0 weights for the fp6-MFMA GEMMs (gemm_f6.hip)
     WPtr qkv_plain;  // head-major QKV in grouped, plain tile order: qkv_attention_kernel's copy (when supported)
     float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
@@ -187,6 +188,7 @@ struct Workspace {
     float *X = nullptr, *out = nullptr;
     uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16: kernels.h GemmArgs EPI_QKV
     ActPtr Xa, Ca, Ua;
+    ActPtr Xd;  // fp6 path: the O + LN output as Q8D (the FFN-up GEMM's input; Xa keeps ggml's Q8_0 for QKV)
     int32_t *tok = nullptr, *off = nullptr, *rowpos = nullptr;
     int32_t *tiles = nullptr;  // qkv_attention_kernel's sentence tiles: [first, count] pairs
     int32_t *perm = nullptr;   // eval_device in tile order: caller's index of each sentence
@@ -247,6 +249,9 @@ struct bert_ctx {
     std::vector<std::unique_ptr<Replica>> reps;
     // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
     bool i8_o = false, i8_up = false, i8_down = false;
+    // Q4_0 models whose O / FFN GEMMs run on the fp6 MFMA (gemm_f6.hip): their
+    // activations are stored as Q8D (kernels.h W_Q4_0D); f6_select
+    bool f6 = false;
     // run_pipeline knobs, read from the environment once at load
     // (BERT_AMD_SPLIT, BERT_AMD_PACK) and changed only by bert_amd_set_option:
     // two row groups on two streams (default on); fused-tile packing
@@ -417,6 +422,46 @@ bool upload_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vec
     return true;
 }
 
+// Repack a Q4_0 [N][K] matrix for the fp6-MFMA GEMMs (kernels.h F6W): per
+// (32-row f-tile, block) each row's 32 codes of q - 8 as e2m3 sign-magnitude
+// 6-bit fields at their Q8D positions (kernels_common.h q8d_pos), split into
+// a 16-byte and an 8-byte plane; the block scales as fp16 in the low half of
+// one dword per block (the d_w operand of the d_w * d_a MFMA).
+bool upload_f6(std::vector<void *> &track, F6W &w, const std::vector<const uint8_t *> &rows, int64_t K) {
+    const int64_t N = (int64_t)rows.size(), nkb = K / 32, nft = N / 32;
+    std::vector<uint32_t> q16((size_t)(N * nkb * 4)), q8((size_t)(N * nkb * 2)), dw((size_t)(N * nkb));
+    for (int64_t ft = 0; ft < nft; ft++)
+        for (int64_t b = 0; b < nkb; b++)
+            for (int m = 0; m < 32; m++) {
+                const uint8_t *blk = rows[(size_t)(32 * ft + m)] + b * 18;
+                uint32_t c6[6] = {0, 0, 0, 0, 0, 0};
+                for (int e = 0; e < 32; e++) {
+                    const uint8_t byte = blk[2 + (e & 15)];
+                    const int v = (e < 16 ? (byte & 15) : (byte >> 4)) - 8;
+                    const uint32_t code = (v < 0 ? 32u : 0u) | (uint32_t)(v < 0 ? -v : v);
+                    const int pos = 8 * (e >> 3) + 2 * (e & 3) + ((e >> 2) & 1);  // kernels_common.h q8d_pos
+                    const int bit = 6 * pos, wd = bit >> 5, o = bit & 31;
+                    c6[wd] |= code << o;
+                    if (o > 26) c6[wd + 1] |= code >> (32 - o);
+                }
+                const size_t i = (size_t)((ft * nkb + b) * 32 + m);
+                for (int k = 0; k < 4; k++) q16[i * 4 + k] = c6[k];
+                q8[i * 2] = c6[4];
+                q8[i * 2 + 1] = c6[5];
+                uint16_t dh;
+                std::memcpy(&dh, blk, 2);
+                dw[(size_t)((((ft * (nkb / 4) + b / 4) * 32) + m) * 4 + (b & 3))] = dh;
+            }
+    void *p16 = nullptr, *p8 = nullptr, *pd = nullptr;
+    if (!upload(track, &p16, q16.data(), q16.size() * 4) || !upload(track, &p8, q8.data(), q8.size() * 4) ||
+        !upload(track, &pd, dw.data(), dw.size() * 4))
+        return false;
+    w.q16 = (const uint4 *)p16;
+    w.q8 = (const uint2 *)p8;
+    w.dw = (const uint4 *)pd;
+    return true;
+}
+
 bool upload_packed(std::vector<void *> &track, WPtr &w, const Packed &p) {
     void *q = nullptr;
     if (!upload(track, &q, p.q.data(), p.q.size())) return false;
@@ -432,8 +477,15 @@ std::vector<const uint8_t *> rows_of(const GGUFTensor *t) {
     return r;
 }
 
-size_t act_elem_bytes(int wtype) { return wtype == W_F32 ? 4 : wtype == W_F16 ? 2 : 1; }
-size_t act_scale_bytes(int wtype) { return wtype == W_Q4_0 ? 2 : wtype == W_Q4_1 ? 4 : 0; }
+// The activation format of the O / FFN GEMM inputs (Ca, Ua, Xd; kernels.h
+// WType).  Xa, the LN output the QKV GEMMs read, is always ctx->wtype's.
+int act_type(const bert_ctx *ctx) { return ctx->f6 ? W_Q4_0D : ctx->wtype; }
+
+// activation format of a row of K values: element / block-scale bytes
+size_t act_row_bytes(int at, int64_t K) {
+    return at == W_Q4_0D ? (size_t)(K / 32) * Q8D_BLK : (size_t)K * (at == W_F32 ? 4 : at == W_F16 ? 2 : 1);
+}
+size_t act_scale_bytes(int at) { return at == W_Q4_0 || at == W_Q4_0D ? 2 : at == W_Q4_1 ? 4 : 0; }
 
 // Activation buffers carry GEMM_BM spare rows: qkv_attention_kernel reads the
 // 128-row tile starting at each sentence's first token (rows past M are
@@ -444,8 +496,8 @@ size_t act_scale_bytes(int wtype) { return wtype == W_Q4_0 ? 2 : wtype == W_Q4_1
 // race it).
 bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, int64_t K, hipStream_t st) {
     rows += GEMM_BM;
-    if (!dmalloc(track, &a.q, (size_t)rows * K * act_elem_bytes(wtype))) return false;
-    HIP_OK(hipMemsetAsync(a.q, 0, (size_t)rows * K * act_elem_bytes(wtype), st));
+    if (!dmalloc(track, &a.q, (size_t)rows * act_row_bytes(wtype, K))) return false;
+    HIP_OK(hipMemsetAsync(a.q, 0, (size_t)rows * act_row_bytes(wtype, K), st));
     if (act_scale_bytes(wtype)) {
         if (!dmalloc(track, &a.d, (size_t)rows * (K / 32) * act_scale_bytes(wtype))) return false;
         HIP_OK(hipMemsetAsync(a.d, 0, (size_t)rows * (K / 32) * act_scale_bytes(wtype), st));
@@ -469,15 +521,16 @@ bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, h
     w.cap_rows = w.cap_seqs = 0;
     w.X = w.out = nullptr;
     w.qk_hi = w.qk_lo = w.vt_hi = w.vt_lo = nullptr;
-    w.Xa = w.Ca = w.Ua = ActPtr{};
+    w.Xa = w.Ca = w.Ua = w.Xd = ActPtr{};
     w.tok = w.off = w.rowpos = w.tiles = w.perm = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
-    const int wt = ctx->wtype;
+    const int at = act_type(ctx);
+    if (ctx->f6 && !alloc_act(w.allocs, w.Xd, W_Q4_0D, rows, E, st)) return false;
     if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
         !dmalloc(w.allocs, &w.qk_lo, (size_t)rows * 2 * E * 2) || !dmalloc(w.allocs, &w.vt_hi, (size_t)rows * E * 2) ||
         !dmalloc(w.allocs, &w.vt_lo, (size_t)rows * E * 2) ||
-        !alloc_act(w.allocs, w.Xa, wt, rows, E, st) || !alloc_act(w.allocs, w.Ca, wt, rows, E, st) ||
-        !alloc_act(w.allocs, w.Ua, wt, rows, I, st) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
+        !alloc_act(w.allocs, w.Xa, ctx->wtype, rows, E, st) || !alloc_act(w.allocs, w.Ca, at, rows, E, st) ||
+        !alloc_act(w.allocs, w.Ua, at, rows, I, st) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
         !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4) ||
         !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4) || !dmalloc(w.allocs, &w.tiles, (size_t)seqs * 2 * 4) ||
         !dmalloc(w.allocs, &w.perm, (size_t)seqs * 4))
@@ -580,6 +633,18 @@ void i8_select(bert_ctx *ctx) {
     ctx->i8_down = q4 && has("down") && i8_gemm_supported(ln, E, I);
 }
 
+// Q4_0 models of n_embd 384 (MiniLM) run the O, FFN-up and FFN-down GEMMs on
+// the fp6 MFMA (gemm_f6.hip: bitwise the int8 path's results, faster), their
+// activations stored as Q8D.  Opt-in for now (env BERT_AMD_F6=1, read at
+// load): in the full pipeline it does not yet beat the int8 kernels.
+void f6_select(bert_ctx *ctx) {
+    const char *e = std::getenv("BERT_AMD_F6");
+    const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
+    ctx->f6 = e && e[0] == '1' && ctx->wtype == W_Q4_0 && E == 384 && f6_gemm_supported(EPI_GELU_ACT, I, E) &&
+              f6_gemm_supported(EPI_LN, E, E) && f6_gemm_supported(EPI_LN, E, I);
+    if (ctx->f6) ctx->i8_o = ctx->i8_up = ctx->i8_down = false;
+}
+
 // One encoder layer over the row group [row0, row0 + rows) (sentences
 // d_off[0 .. nseq), absolute row offsets).  Xa / Ca / Ua / X point at the
 // group's first row; the QKV + attention kernels index rows absolutely through
@@ -587,7 +652,7 @@ void i8_select(bert_ctx *ctx) {
 // with one group, row0 == 0).
 bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
                const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
-               ActPtr Ca, ActPtr Ua, float *X, hipStream_t st) {
+               ActPtr Ca, ActPtr Ua, ActPtr Xd, float *X, hipStream_t st) {
     const HParams &hp = ctx->hp;
     Workspace &w = R.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
@@ -625,10 +690,46 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, st));
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(ctx->f6 ? W_Q4_0D : wt, qf, aa, ntiles, st));
         } else {
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
-            LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
+            LAUNCH_OK("attention", launch_attention(act_type(ctx), D, aa, nseq, max_len, st));
+        }
+        if (ctx->f6) {  // O + LN, FFN up + GELU, FFN down + LN on the fp6 MFMA, Q8D in
+            GemmArgs o;
+            o.A = Ca;
+            o.K = E;
+            o.N = E;
+            o.Wf = L.o6;
+            o.bias = L.b_o;
+            o.X = X;
+            o.out_act = Xd;
+            o.ln_w = L.ln1_w;
+            o.ln_b = L.ln1_b;
+            o.eps = hp.eps;
+            LAUNCH_OK("gemm_o_ln", launch_gemm_f6(EPI_LN, o, (int)rows, st, W_Q4_0D));
+            GemmArgs u;
+            u.A = Xd;
+            u.K = E;
+            u.N = I;
+            u.Wf = L.up6;
+            u.bias = L.b_up;
+            u.out_act = Ua;
+            u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
+            LAUNCH_OK("gemm_up_gelu", launch_gemm_f6(EPI_GELU_ACT, u, (int)rows, st, W_Q4_0D));
+            GemmArgs dn;
+            dn.A = Ua;
+            dn.K = I;
+            dn.N = E;
+            dn.Wf = L.down6;
+            dn.bias = L.b_down;
+            dn.X = X;
+            dn.out_act = Xa;
+            dn.ln_w = L.ln2_w;
+            dn.ln_b = L.ln2_b;
+            dn.eps = hp.eps;
+            LAUNCH_OK("gemm_down_ln", launch_gemm_f6(EPI_LN, dn, (int)rows, st, W_Q4_0));  // next layer's QKV input
+            return true;
         }
 
         GemmArgs o;
@@ -747,7 +848,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     const bool fused_qkv_attn = !force_unfused && qkv_attention_supported(wt, E, H, max_len);
 
     const EmbedArgs ea = embed_args(ctx, R, d_tok, d_off, n_seqs, M);
-    LAUNCH_OK("embed_ln", launch_embed(wt, ea, (int)Mpad, st));
+    LAUNCH_OK("embed_ln", launch_embed(ctx->wtype, ea, (int)Mpad, st));
 
     // Row groups (default; ctx->split = 0 turns them off):
     // with the fused QKV + attention path the batch is split at a 128-row-aligned
@@ -813,19 +914,21 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
             HIP_OK(hipStreamWaitEvent(R.stream2, R.ev_fork, 0));
         }
     }
-    const size_t eb = act_elem_bytes(wt), sb = act_scale_bytes(wt);
-    auto act_rows = [&](ActPtr a, int64_t row0, int64_t K) {
-        a.q = (char *)a.q + row0 * K * (int64_t)eb;
-        if (a.d) a.d = (char *)a.d + row0 * (K / 32) * (int64_t)sb;
+    auto act_rows = [&](ActPtr a, int at, int64_t row0, int64_t K) {
+        if (!a.q) return a;
+        a.q = (char *)a.q + row0 * (int64_t)act_row_bytes(at, K);
+        if (a.d) a.d = (char *)a.d + row0 * (K / 32) * (int64_t)act_scale_bytes(at);
         return a;
     };
+    const int at = act_type(ctx);
 
     for (int il = 0; il < hp.n_layer; il++)
         for (int gi = 0; gi < ng; gi++) {
             const Group &gr = G[gi];
             if (!run_layer(ctx, R, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, w.tiles + 2 * gr.seq0, ntl[gi],
-                           max_len, fused_qkv_attn, ln_fused, act_rows(w.Xa, gr.row0, E), act_rows(w.Ca, gr.row0, E),
-                           act_rows(w.Ua, gr.row0, I), w.X + gr.row0 * E, gr.s))
+                           max_len, fused_qkv_attn, ln_fused, act_rows(w.Xa, wt, gr.row0, E),
+                           act_rows(w.Ca, at, gr.row0, E), act_rows(w.Ua, at, gr.row0, I),
+                           act_rows(w.Xd, W_Q4_0D, gr.row0, E), w.X + gr.row0 * E, gr.s))
                 return false;
         }
     if (ng == 2) {
@@ -976,8 +1079,12 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                     for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
         }
         if (!upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
-        // each projection in the one format its GEMM reads (int8 or split fp16)
-        if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E))) ||
+        // each projection in the one format its GEMM reads (fp6, int8 or split fp16)
+        if (ctx->f6) {
+            if (!upload_f6(tr, dl.o6, rows_of(l.o_w), E) || !upload_f6(tr, dl.up6, rows_of(l.i_w), E) ||
+                !upload_f6(tr, dl.down6, rows_of(l.o2_w), I))
+                return false;
+        } else if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E))) ||
             !(ctx->i8_up ? upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) : upload_packed(tr, dl.up, repack(wt, up_rows, E))) ||
             !(ctx->i8_down ? upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I)
                            : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))))
@@ -1153,6 +1260,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
         return nullptr;
     }
     i8_select(ctx.get());
+    f6_select(ctx.get());
     if (const char *e = std::getenv("BERT_AMD_SPLIT")) ctx->split = e[0] != '0';
     if (const char *e = std::getenv("BERT_AMD_PACK")) ctx->pack = e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
     // devices
@@ -1694,7 +1802,7 @@ int32_t bert_amd_debug_embed(bert_ctx *ctx, const int32_t *tokens, const int32_t
         HIP_OK_RC(launch_embed(ctx->wtype, ea, (int)Mpad, st), -4);
         const int64_t E = ctx->hp.n_embd;
         HIP_OK_RC(hipMemcpyAsync(X_out, w.X, (size_t)(M * E) * 4, hipMemcpyDeviceToHost, st), -3);
-        HIP_OK_RC(hipMemcpyAsync(q_out, w.Xa.q, (size_t)(M * E) * act_elem_bytes(ctx->wtype), hipMemcpyDeviceToHost, st), -3);
+        HIP_OK_RC(hipMemcpyAsync(q_out, w.Xa.q, (size_t)M * act_row_bytes(ctx->wtype, E), hipMemcpyDeviceToHost, st), -3);
         if (d_out && act_scale_bytes(ctx->wtype))
             HIP_OK_RC(hipMemcpyAsync(d_out, w.Xa.d, (size_t)(M * (E / 32)) * act_scale_bytes(ctx->wtype),
                                      hipMemcpyDeviceToHost, st), -3);

@@ -130,6 +130,30 @@ def test_int8_gemm_path_golden(case, mode, model_dir, monkeypatch):
     assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
 
 
+@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01"])
+def test_fp6_gemm_path_bitwise_int8(case, model_dir, monkeypatch):
+    """O / FFN-up / FFN-down on the fp6-MFMA GEMMs (env BERT_AMD_F6=1:
+    gemm_f6.hip, Q8D activations, isum as two exact fp6 digit-plane MFMAs,
+    the same per-block fold as gemm_i8.hip): the golden fixtures within the
+    bound, and bitwise the int8-MFMA path's embeddings (BERT_AMD_I8=1)."""
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    outs = {}
+    for f6 in ("1", "0"):
+        monkeypatch.setenv("BERT_AMD_F6", f6)
+        monkeypatch.setenv("BERT_AMD_I8", "1")
+        m = bertlib.BertModel(p)  # fresh context: both are read at load
+        try:
+            outs[f6] = m.eval_batch(toks)
+            assert np.array_equal(outs[f6], m.eval_batch(toks))
+        finally:
+            m.close()
+    c = cos(outs["1"], want)
+    print(f"BERT_AMD_F6=1 {case}: 1-cos max {1 - c.min():.2e}")
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
+    assert np.array_equal(outs["1"], outs["0"])
+
+
 def test_batch_invariance_and_determinism(model_dir):
     p, m = get_model(model_dir, "minilm", "q4_0")
     toks = [sentence(i, n, 30522) for i, n in enumerate([5, 128, 64, 17, 512, 128])]
