@@ -71,7 +71,7 @@ def max_over_ranks(x: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -137,6 +137,71 @@ KERNEL_SYMBOL = {
 }
 
 
+def consumer_line(model, hp, n_texts, rank, dev, stream, torch):
+    import ctypes
+    L = model.lib
+    words = []
+    for i in range(1000, hp["n_vocab"]):
+        w = L.bert_vocab_id_to_token(model.ctx, i).decode("utf-8", "replace")
+        if w.isalpha() and w.islower() and not w.startswith("##"):
+            words.append(w)
+    rng = np.random.default_rng(SEED + 7 + rank)
+    lens = rng.integers(8, 129, n_texts)  # framed token counts: [CLS] + words + [SEP]
+    texts = [" ".join(rng.choice(words, n - 2)) for n in lens]
+    n = len(texts)
+    c_texts = (ctypes.c_char_p * n)(*[t.encode("utf-8") for t in texts])
+    # tokeniser alone (bert_tokenize per text through ctypes, one thread)
+    buf = (ctypes.c_int32 * hp["n_max_tokens"])()
+    nt = ctypes.c_int32(0)
+    t0 = time.perf_counter()
+    toks = []
+    for i in range(n):
+        L.bert_tokenize(model.ctx, c_texts[i], buf, ctypes.byref(nt), hp["n_max_tokens"])
+        toks.append(np.frombuffer(buf, np.int32, nt.value).copy())
+    t_tok = time.perf_counter() - t0
+    ntoks = np.array([len(t) for t in toks])
+    framed_ok = bool(np.array_equal(ntoks, lens))
+    emb = np.zeros((n, hp["n_embd"]), np.float32)
+    ptrs = (bertlib.F_P * n)(*[emb[i].ctypes.data_as(bertlib.F_P) for i in range(n)])
+    threads = int(os.environ.get("OMP_NUM_THREADS", 0) or 8)
+    res = dict(texts=n, mean_tokens=round(float(ntoks.mean()), 2), lengths="uniform 8..128 tokens (seeded)",
+               framing_ok=framed_ok, n_threads=threads,
+               tokenizer=dict(texts_per_s=round(n / t_tok, 1), tokens_per_s=round(float(ntoks.sum()) / t_tok, 1),
+                              note="bert_tokenize per text via ctypes, one thread"))
+    ref = None
+    for bs in (16, 256, n):
+        L.bert_encode_batch(model.ctx, threads, bs, n, c_texts, ptrs)  # warm-up (workspace growth)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            L.bert_encode_batch(model.ctx, threads, bs, n, c_texts, ptrs)
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        if ref is None:
+            ref = emb.copy()
+        res[f"encode_batch_{'all' if bs == n else bs}"] = dict(value=round(n / med, 1), unit="embeddings/s",
+                                                              ms_median=round(med * 1e3, 2),
+                                                              bitwise_vs_batch16=bool(np.array_equal(emb, ref)))
+    # the same sentences device-resident, one batch (eval_device)
+    offs = np.zeros(n + 1, np.int32)
+    offs[1:] = np.cumsum(ntoks)
+    d_tok = torch.from_numpy(np.concatenate(toks)).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_out = torch.empty(n, hp["n_embd"], dtype=torch.float32, device=dev)
+    for _ in range(2):
+        model.eval_device(d_tok.data_ptr(), d_off.data_ptr(), offs, n, d_out.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        model.eval_device(d_tok.data_ptr(), d_off.data_ptr(), offs, n, d_out.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    dres = n * 5 / (time.perf_counter() - t0)
+    res["device_resident_same_sentences"] = dict(value=round(dres, 1), unit="embeddings/s")
+    res["batch16_frac_of_device"] = round(res["encode_batch_16"]["value"] / dres, 4)
+    res["bitwise_vs_device"] = bool(np.array_equal(d_out.cpu().numpy(), ref))
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -154,6 +219,12 @@ def main():
     ap.add_argument("--pmc-csv", default=os.environ.get("BENCH_PMC_CSV", ""))
     ap.add_argument("--host-runs", type=int, default=10, help="timed bert_eval_batch runs (host buffers), 0: skip")
     ap.add_argument("--ragged-steps", type=int, default=10, help="variable-length batch steps, 0: skip")
+    ap.add_argument("--consumer-texts", type=int, default=4096,
+                    help="texts for the bert_encode_batch (consumer path) line, 0: skip")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="development: every rank on device 0, gloo instead of RCCL (N > 1 code paths on a 1-GPU box)")
+    ap.add_argument("--lib-shard", type=int, default=1,
+                    help="N>1: rank 0 also times the library's own sharding (bert_amd_load over all N devices)")
     args = ap.parse_args()
 
     import torch
@@ -163,11 +234,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = 0 if args.rehearse_one_gpu else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
         if world > 1:
@@ -191,7 +266,7 @@ def main():
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        model = bertlib.BertModel(path, devices=[local_rank])
+        model = bertlib.BertModel(path, devices=[gpu])
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -357,6 +432,16 @@ def main():
                                   unit_norm=bool(np.allclose(np.linalg.norm(remb, axis=1), 1.0, atol=1e-5)),
                                   note="bert_eval_batch, host buffers, same lengths")
 
+    # the reference consumers' path (examples/sample_dylib.py:42 batch 16,
+    # benchmarks/run_mteb.py:19,89 batch os.cpu_count()): bert_encode_batch on
+    # synthetic texts of whole vocabulary words (one token each, 8..128 tokens
+    # framed), host tokenisation and host buffers included, against the same
+    # sentences device-resident in one batch
+    consumer = None
+    if args.consumer_texts > 0:
+        log("consumer path timing (bert_encode_batch)")
+        consumer = consumer_line(model, hp, args.consumer_texts, rank, dev, stream, torch)
+
     cpu = None
     parity = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -390,6 +475,44 @@ def main():
         parity = dict(cos_min=float(c.min()), cos_mean=float(c.mean()), n=S,
                       max_abs=float(np.abs(out[:S] - ref).max()))
 
+    # N > 1: the library's own sharding, the path drop-in consumers get
+    # (bert_amd_load over every device of the node + bert_eval_batch on host
+    # buffers: one thread per device, slices balanced by token count), on the
+    # global batch world x B; rank 0 only, the other ranks idle on the CPU
+    lib_shard = None
+    if world > 1 and args.lib_shard:
+        flag = f"/tmp/bert_amd_libshard_{os.environ.get('MASTER_PORT', '0')}.done"
+        if rank == 0:
+            log(f"library sharding over {world} devices")
+            gm = bertlib.BertModel(path, devices=[0] * world if args.rehearse_one_gpu else list(range(world)))
+            try:
+                gtoks = splitmix_tokens(0, world * B, N, hp["n_vocab"])
+                run, gemb = gm.prepared_batch(list(gtoks))
+                for _ in range(2):
+                    run()
+                ts = []
+                for _ in range(5):
+                    t0 = time.perf_counter()
+                    run()
+                    ts.append(time.perf_counter() - t0)
+                med = float(np.median(ts))
+                lib_shard = dict(value=round(world * B / med, 1), unit="embeddings/s", devices=gm.n_devices,
+                                 workload=f"{args.shape} {args.ftype} global batch={world * B} seq_len={N}",
+                                 ms_median=round(med * 1e3, 3), runs=5,
+                                 bitwise_vs_rank0=bool(np.array_equal(gemb[:B], out)),
+                                 note="bert_amd_load(devices=0..N-1) + bert_eval_batch on host buffers "
+                                      "(H2D ids and D2H embeddings included)")
+            finally:
+                gm.close()
+                with open(flag, "w") as f:
+                    f.write("done")
+        else:
+            while not os.path.exists(flag):
+                time.sleep(0.05)
+        barrier()
+        if rank == 0:
+            os.remove(flag)
+
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(value, 1), "unit": "embeddings/s", "n_gpus": world,
@@ -414,6 +537,8 @@ def main():
             "host_api": host_api,
             "ragged": ragged,
             "ragged_short": ragged_short,
+            "consumer": consumer,
+            "library_sharding": lib_shard,
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)

@@ -53,6 +53,21 @@ constexpr int F6_UP_NMAX = 4096;                          // FFN-up width held i
 // development ablations (tools/f6_bench.hip only; results wrong): bit 1 no
 // fold, 2 no dd MFMA, 4 no fp6 MFMA, 8 no weight loads, 16 no A-operand LDS
 // reads, 32 no epilogue (one checksum store per lane and tile)
+// development: every other CU of an XCD starts F6_DESYNC_UP / _LN shader
+// cycles late, so the workgroups' HBM-bound epilogues stop coinciding
+#ifndef F6_DESYNC_UP
+#define F6_DESYNC_UP 0
+#endif
+#ifndef F6_DESYNC_LN
+#define F6_DESYNC_LN 0
+#endif
+__device__ __forceinline__ void f6_desync(int cycles) {
+    if (cycles > 0 && ((blockIdx.x >> 3) & 1)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)cycles) __builtin_amdgcn_s_sleep(8);
+    }
+}
+
 #ifndef F6_ABL
 #define F6_ABL 0
 #endif
@@ -353,12 +368,13 @@ __global__ __launch_bounds__(NWV * 64) void f6_up_gelu_kernel(GemmArgs g, int n_
     constexpr int NT = NWV * 64, BM = 32 * T, BN = 32 * NWV * F;
     using C = F6Chunk<BM>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
-    __shared__ __attribute__((aligned(16))) uint16_t gtab[GELU_FLAT_LDS];
+    __shared__ __attribute__((aligned(16))) uint16_t gtab[(F6_ABL & 32) ? 8 : GELU_FLAT_LDS];
     __shared__ __attribute__((aligned(16))) float sbias[F6_UP_NMAX];  // the epilogue reads bias from LDS
     const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile coordinates in SGPRs
     const int nflat8 = (0x8000 + g.gelu.neg_n + 1 + 7) / 8;
-    for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)g.gelu.full)[i];
+    if constexpr ((F6_ABL & 32) == 0)
+        for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)g.gelu.full)[i];
     for (int i = tid; i < g.N; i += NT) sbias[i] = g.bias[i];
     const float xlo = h2f((uint16_t)(0x8000 | g.gelu.neg_n));
     const int nwg = n_mtiles * n_ntiles, nbo = g.N >> 5;
@@ -370,6 +386,7 @@ __global__ __launch_bounds__(NWV * 64) void f6_up_gelu_kernel(GemmArgs g, int n_
         ft0_ = nt * (BN / 32) + fw;
     };
     if ((int)blockIdx.x >= nwg) return;
+    f6_desync(F6_DESYNC_UP);
     int64_t m0;
     int ft0;
     coords(blockIdx.x, m0, ft0);
@@ -411,7 +428,8 @@ __global__ __launch_bounds__(NWV * 64) void f6_up_gelu_kernel(GemmArgs g, int n_
 #pragma unroll
                 for (int i = 0; i < 16; i++) y[i] = h2f(gtab[f2h(fmaxf(bias[i] + acc[f][t][i], xlo))]);
                 const int64_t bi = (mc + 32 * t + l32) * nbo + fc + f;
-                q8d_store_pair((char *)g.out_act.q + bi * Q8D_BLK, (uint16_t *)g.out_act.d + bi, hh, y);
+                q8d_store_pair((char *)g.out_act.q + bi * Q8D_BLK, (uint16_t *)g.out_act.d + bi, hh, y,
+                               (F6_ABL & 64) == 0 || g.eps == 12345.f);
             }
         }
     }
@@ -428,7 +446,8 @@ __global__ __launch_bounds__(NWV * 64) void f6_up_gelu_kernel(GemmArgs g, int n_
 // natural-order accumulator layout (element 4q + j of lane half hh is column
 // 8q + 4hh + j), stored as ggml's Q8_0 (int8 codes + fp16 d; the i8 path's
 // i8_store_q8_half arithmetic): four dwords per lane.
-__device__ __forceinline__ void f6_store_q8_0(const ActPtr &out, int64_t row, int blk, int hh, const float (&y)[16]) {
+__device__ __forceinline__ void f6_store_q8_0(const ActPtr &out, int64_t row, int blk, int hh, const float (&y)[16],
+                                              bool valid = true) {
     float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; i++) amax = fmaxf(amax, fabsf(y[i]));
@@ -439,8 +458,12 @@ __device__ __forceinline__ void f6_store_q8_0(const ActPtr &out, int64_t row, in
     float d, id;
     q8_scales(amax, d, id);
     uint32_t *dst = (uint32_t *)((int8_t *)out.q + row * 384 + 32 * blk + 4 * hh);
+    uint32_t pk[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) dst[2 * q] = q8_pack4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3], id);
+    for (int q = 0; q < 4; q++) pk[q] = q8_pack4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3], id);
+    if (!valid) return;
+#pragma unroll
+    for (int q = 0; q < 4; q++) dst[2 * q] = pk[q];
     if (hh == 0) ((uint16_t *)out.d)[row * 12 + blk] = f2h(d);
 }
 
@@ -458,6 +481,7 @@ __global__ __launch_bounds__(768) void f6_ln384_kernel(GemmArgs g, int n_mtiles)
         prm[k][c] = (k == 0 ? g.bias : k == 1 ? g.ln_w : g.ln_b)[c];
     }
     if ((int)blockIdx.x >= n_mtiles) return;
+    f6_desync(F6_DESYNC_LN);
     int64_t m0n = (int64_t)f6_xcd_linear(blockIdx.x, n_mtiles) * BM;
     F6Pipe<NT, BM, F, F6_LN_WR> pp;
     pp.prime(g, m0n, ft0);
@@ -540,13 +564,15 @@ __global__ __launch_bounds__(768) void f6_ln384_kernel(GemmArgs g, int n_mtiles)
                     z = w4[j] * z;
                     y[4 * q + j] = z + b4[j];
                 }
-                *(float4v *)(xr + 8 * q) = float4v{y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]};
+                if ((F6_ABL & 64) == 0 || g.eps == 12345.f)
+                    *(float4v *)(xr + 8 * q) = float4v{y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]};
             }
             const int64_t bi = row * NBO + ft0;
             if constexpr (OUT_Q8D)
-                q8d_store_pair((char *)g.out_act.q + bi * Q8D_BLK, (uint16_t *)g.out_act.d + bi, hh, y);
+                q8d_store_pair((char *)g.out_act.q + bi * Q8D_BLK, (uint16_t *)g.out_act.d + bi, hh, y,
+                               (F6_ABL & 64) == 0 || g.eps == 12345.f);
             else
-                f6_store_q8_0(g.out_act, row, ft0, hh, y);
+                f6_store_q8_0(g.out_act, row, ft0, hh, y, (F6_ABL & 64) == 0 || g.eps == 12345.f);
         }
         // the next tile's main loop reuses `red` only after its own barriers
     }
@@ -613,7 +639,10 @@ static int n_cus_f6() {
 
 static int f6_persistent_grid(int tiles) { return std::max(1, std::min(tiles, std::max(8, n_cus_f6() / 8 * 8))); }
 
-constexpr int F6_UP_WAVES = 8, F6_UP_F = 2, F6_UP_T = 2;
+#ifndef F6_UP_FT
+#define F6_UP_FT 22  // f-tiles x t-tiles per wave (development: 14 = F 1, T 4)
+#endif
+constexpr int F6_UP_WAVES = 8, F6_UP_F = F6_UP_FT / 10, F6_UP_T = F6_UP_FT % 10;
 
 bool f6_gemm_supported(int epi, int N, int K) {
     if (K != 384 && K != 1536) return false;  // the chunk loops are unrolled per K

@@ -205,8 +205,11 @@ struct ProfEntry {
     int64_t n = 0;
 };
 
-struct Replica {
-    int device = 0;
+// One evaluation lane of a replica: a workspace with its streams and events.
+// Lane 0 serves bert_eval_batch, eval_device and debug_embed; bert_encode_batch
+// adds lanes (encode_lanes) to run several of its slices at once on one
+// device, each lane's slices in its own host thread and streams.
+struct Lane {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;               // second row group (run_pipeline)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -215,14 +218,20 @@ struct Replica {
     // stream (the library's, a caller's, the null stream) never rewrites
     // buffers an earlier call on another stream is still reading
     hipEvent_t ev_free = nullptr;
+    Workspace ws;
+};
+
+struct Replica {
+    int device = 0;
+    std::vector<std::unique_ptr<Lane>> lanes;  // lanes[0] exists once built
     void *word = nullptr, *pos = nullptr, *type = nullptr;
     float *ln_e_w = nullptr, *ln_e_b = nullptr;
     std::vector<DevLayer> L;
     uint16_t *gelu_tab = nullptr, *exp_tab = nullptr, *gelu_compact = nullptr, *exp_compact = nullptr;
     std::vector<void *> weight_allocs;
-    Workspace ws;
     // profiling: events recorded around each launch when enabled
     bool prof = false;
+    std::mutex prof_mu;  // lanes launch from several host threads
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::map<std::string, ProfEntry> prof_acc;
 };
@@ -255,8 +264,13 @@ struct bert_ctx {
     // run_pipeline knobs, read from the environment once at load
     // (BERT_AMD_SPLIT, BERT_AMD_PACK) and changed only by bert_amd_set_option:
     // two row groups on two streams (default on); fused-tile packing
-    // -1 = when it pays (default), 0 = never, 1 = always
-    int split = 1, pack = -1;
+    // -1 = when it pays (default), 0 = never, 1 = always; batches of fewer than
+    // fuse_min sentences skip the fused QKV + attention kernel (one workgroup per
+    // sentence: its latency, not the chip, bounds a small batch) for the unfused
+    // pair, whose GEMM and attention spread a sentence over many workgroups
+    int split = 1, pack = -1, fuse_min = 48;
+    // bert_encode_batch: slices evaluated at once per device (lanes), >= 1
+    int encode_lanes = 4;
     std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
 };
 
@@ -509,8 +523,8 @@ bool alloc_act(std::vector<void *> &track, ActPtr &a, int wtype, int64_t rows, i
 // still be in use on any stream of the device (the library's or a caller's),
 // so the device is drained before they are freed; the zero-fill of the new
 // ones is issued on `st`, the stream the kernels that use them run on.
-bool ensure_workspace(bert_ctx *ctx, Replica &R, int64_t Mpad, int64_t n_seqs, hipStream_t st) {
-    Workspace &w = R.ws;
+bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hipStream_t st) {
+    Workspace &w = ln.ws;
     if (Mpad <= w.cap_rows && n_seqs <= w.cap_seqs) return true;
     HIP_OK(hipDeviceSynchronize());
     const int64_t rows = std::max<int64_t>(Mpad, w.cap_rows), seqs = std::max<int64_t>(n_seqs, w.cap_seqs);
@@ -562,12 +576,14 @@ struct Launch {
     ~Launch() {
         if (R.prof) {
             hipEventRecord(e1, s);
+            std::lock_guard<std::mutex> lk(R.prof_mu);
             R.pending.push_back({name, {e0, e1}});
         }
     }
 };
 
 void drain_profile(Replica &R) {
+    std::lock_guard<std::mutex> lk(R.prof_mu);
     for (auto &p : R.pending) {
         hipEventSynchronize(p.second.second);
         float ms = 0;
@@ -584,12 +600,12 @@ void drain_profile(Replica &R) {
 // Workspace hand-over between evals (Replica::ev_free): an eval's first
 // device operation waits for the previous eval's last one, whatever streams
 // the two ran on; the eval records the event behind its own last operation.
-bool ws_acquire(Replica &R, hipStream_t st) {
-    HIP_OK(hipStreamWaitEvent(st, R.ev_free, 0));
+bool ws_acquire(Lane &ln, hipStream_t st) {
+    HIP_OK(hipStreamWaitEvent(st, ln.ev_free, 0));
     return true;
 }
-bool ws_release(Replica &R, hipStream_t st) {
-    HIP_OK(hipEventRecord(R.ev_free, st));
+bool ws_release(Lane &ln, hipStream_t st) {
+    HIP_OK(hipEventRecord(ln.ev_free, st));
     return true;
 }
 
@@ -650,11 +666,11 @@ void f6_select(bert_ctx *ctx) {
 // group's first row; the QKV + attention kernels index rows absolutely through
 // the offsets, so they get the workspace bases (the unfused pair only runs
 // with one group, row0 == 0).
-bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
+bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
                const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
                ActPtr Ca, ActPtr Ua, ActPtr Xd, float *X, hipStream_t st) {
     const HParams &hp = ctx->hp;
-    Workspace &w = R.ws;
+    Workspace &w = ln.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
     if (!fused_qkv_attn && row0 != 0) {
         set_err("internal: unfused attention with a row split");
@@ -805,13 +821,13 @@ bool run_layer(bert_ctx *ctx, Replica &R, int il, int64_t row0, int64_t rows, co
 }
 
 // embed_ln's arguments for a batch resident in the replica's workspace
-EmbedArgs embed_args(const bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, int n_seqs,
+EmbedArgs embed_args(const bert_ctx *ctx, Replica &R, const Workspace &w, const int32_t *d_tok, const int32_t *d_off, int n_seqs,
                      int64_t M) {
     const HParams &hp = ctx->hp;
     EmbedArgs ea;
     ea.tokens = d_tok;
     ea.offsets = d_off;
-    ea.rowpos = R.ws.rowpos;
+    ea.rowpos = w.rowpos;
     ea.n_seqs = n_seqs;
     ea.M = (int)M;
     ea.E = hp.n_embd;
@@ -824,30 +840,30 @@ EmbedArgs embed_args(const bert_ctx *ctx, Replica &R, const int32_t *d_tok, cons
     ea.ln_w = R.ln_e_w;
     ea.ln_b = R.ln_e_b;
     ea.eps = hp.eps;
-    ea.X = R.ws.X;
-    ea.Xa = R.ws.Xa;
+    ea.X = w.X;
+    ea.Xa = w.Xa;
     return ea;
 }
 
 // The fixed pipeline over a ragged batch already resident on the device.
 // d_out_row (optional): output row of each sentence of the batch.
-bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
+bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
                   int n_seqs, float *d_out, hipStream_t st, const int32_t *d_out_row = nullptr) {
     const HParams &hp = ctx->hp;
     const int64_t M = h_off[n_seqs];
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
     int max_len = 0;
     for (int s = 0; s < n_seqs; s++) max_len = std::max(max_len, h_off[s + 1] - h_off[s]);
-    if (!ensure_workspace(ctx, R, Mpad, n_seqs, st)) return false;
-    Workspace &w = R.ws;
+    if (!ensure_workspace(ctx, ln, Mpad, n_seqs, st)) return false;
+    Workspace &w = ln.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, wt = ctx->wtype;
     const bool ln_fused = gemm_ln_fused(wt, E);
     // QKV + attention in one kernel when every sentence fits one 128-row tile
     // (env BERT_AMD_UNFUSED=1 forces the two-kernel path, for A/B checks)
     static const bool force_unfused = std::getenv("BERT_AMD_UNFUSED") != nullptr;
-    const bool fused_qkv_attn = !force_unfused && qkv_attention_supported(wt, E, H, max_len);
+    const bool fused_qkv_attn = !force_unfused && n_seqs >= ctx->fuse_min && qkv_attention_supported(wt, E, H, max_len);
 
-    const EmbedArgs ea = embed_args(ctx, R, d_tok, d_off, n_seqs, M);
+    const EmbedArgs ea = embed_args(ctx, R, w, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(ctx->wtype, ea, (int)Mpad, st));
 
     // Row groups (default; ctx->split = 0 turns them off):
@@ -869,7 +885,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     };
     Group G[2] = {{0, Mpad, 0, n_seqs, st}, {0, 0, 0, 0, nullptr}};
     int ng = 1;
-    if (ctx->split && fused_qkv_attn && ln_fused && n_seqs >= 512 && R.stream2) {
+    if (ctx->split && fused_qkv_attn && ln_fused && n_seqs >= 512 && ln.stream2) {
         int best = -1;
         for (int s = 1; s < n_seqs; s++)
             if (h_off[s] % GEMM_BM == 0 &&
@@ -877,10 +893,10 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
                 best = s;
         if (best > 0 && 4LL * h_off[best] >= M && 4LL * h_off[best] <= 3 * M) {
             G[0] = {0, h_off[best], 0, best, st};
-            G[1] = {h_off[best], Mpad - h_off[best], best, n_seqs - best, R.stream2};
+            G[1] = {h_off[best], Mpad - h_off[best], best, n_seqs - best, ln.stream2};
             ng = 2;
-            HIP_OK(hipEventRecord(R.ev_fork, st));
-            HIP_OK(hipStreamWaitEvent(R.stream2, R.ev_fork, 0));
+            HIP_OK(hipEventRecord(ln.ev_fork, st));
+            HIP_OK(hipStreamWaitEvent(ln.stream2, ln.ev_fork, 0));
         }
     }
     // Sentence tiles for the fused kernel: consecutive sentences packed greedily
@@ -900,6 +916,12 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
             for (int s = G[gi].seq0, e = G[gi].seq0 + G[gi].nseq; s < e;) {
                 int k = s + 1, used = span(s);
                 while (!no_pack && k < e && used + span(k) <= GEMM_BM) used += span(k++);
+                // the packed kernel's contract (kernels.hip qkv_attention_kernel returns
+                // without writing on a tile of more than 4 sentences or 128 rows)
+                if (k - s > 4 || used > GEMM_BM) {
+                    set_err("internal: sentence tile of %d sentences / %d rows", k - s, used);
+                    return false;
+                }
                 t[2 * ntl[gi]] = s - G[gi].seq0;
                 t[2 * ntl[gi] + 1] = k - s;
                 ntl[gi]++;
@@ -910,8 +932,8 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
         // pageable source: the copy is staged before the call returns, so ht may be reused
         HIP_OK(hipMemcpyAsync(w.tiles, ht.data(), (size_t)2 * n_seqs * 4, hipMemcpyHostToDevice, st));
         if (ng == 2) {
-            HIP_OK(hipEventRecord(R.ev_fork, st));
-            HIP_OK(hipStreamWaitEvent(R.stream2, R.ev_fork, 0));
+            HIP_OK(hipEventRecord(ln.ev_fork, st));
+            HIP_OK(hipStreamWaitEvent(ln.stream2, ln.ev_fork, 0));
         }
     }
     auto act_rows = [&](ActPtr a, int at, int64_t row0, int64_t K) {
@@ -925,15 +947,15 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, const int32_t *d_tok, const int32_t
     for (int il = 0; il < hp.n_layer; il++)
         for (int gi = 0; gi < ng; gi++) {
             const Group &gr = G[gi];
-            if (!run_layer(ctx, R, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, w.tiles + 2 * gr.seq0, ntl[gi],
+            if (!run_layer(ctx, R, ln, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, w.tiles + 2 * gr.seq0, ntl[gi],
                            max_len, fused_qkv_attn, ln_fused, act_rows(w.Xa, wt, gr.row0, E),
                            act_rows(w.Ca, at, gr.row0, E), act_rows(w.Ua, at, gr.row0, I),
                            act_rows(w.Xd, W_Q4_0D, gr.row0, E), w.X + gr.row0 * E, gr.s))
                 return false;
         }
     if (ng == 2) {
-        HIP_OK(hipEventRecord(R.ev_join, R.stream2));
-        HIP_OK(hipStreamWaitEvent(st, R.ev_join, 0));
+        HIP_OK(hipEventRecord(ln.ev_join, ln.stream2));
+        HIP_OK(hipStreamWaitEvent(st, ln.ev_join, 0));
     }
     LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st, d_out_row));
     return true;
@@ -1013,14 +1035,22 @@ std::vector<float> table_f32(const GGUFTensor *t) {
     return out;
 }
 
+// A new lane on R's device (the caller has set it current)
+bool add_lane(Replica &R) {
+    auto ln = std::make_unique<Lane>();
+    HIP_OK(hipStreamCreateWithFlags(&ln->stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&ln->stream2, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&ln->ev_fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ln->ev_join, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ln->ev_free, hipEventDisableTiming));
+    R.lanes.push_back(std::move(ln));
+    return true;
+}
+
 bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
     R.device = device;
     HIP_OK(hipSetDevice(device));
-    HIP_OK(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&R.stream2, hipStreamNonBlocking));
-    HIP_OK(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&R.ev_free, hipEventDisableTiming));
+    if (!add_lane(R)) return false;
     auto &tr = R.weight_allocs;
     const std::vector<float> word = table_f32(hm.word), pos = table_f32(hm.pos), type = table_f32(hm.type);
     if (!upload(tr, &R.word, word.data(), word.size() * 4) || !upload(tr, &R.pos, pos.data(), pos.size() * 4) ||
@@ -1101,24 +1131,23 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
 }
 
 void free_replica(Replica &R) {
-    if (R.stream) {
-        hipSetDevice(R.device);
-        hipDeviceSynchronize();  // caller streams may still read the workspace
-    }
+    hipSetDevice(R.device);
+    hipDeviceSynchronize();  // caller streams may still read the workspace
     drain_profile(R);
-    for (void *p : R.ws.allocs) hipFree(p);
-    for (void *p : R.weight_allocs) hipFree(p);
-    if (R.ws.h_tok) hipHostFree(R.ws.h_tok);
-    if (R.ws.h_off) hipHostFree(R.ws.h_off);
-    if (R.ws.h_out) hipHostFree(R.ws.h_out);
-    if (R.stream2) {
-        hipStreamSynchronize(R.stream2);
-        hipStreamDestroy(R.stream2);
+    for (auto &lp : R.lanes) {
+        Lane &ln = *lp;
+        for (void *p : ln.ws.allocs) hipFree(p);
+        if (ln.ws.h_tok) hipHostFree(ln.ws.h_tok);
+        if (ln.ws.h_off) hipHostFree(ln.ws.h_off);
+        if (ln.ws.h_out) hipHostFree(ln.ws.h_out);
+        if (ln.stream2) hipStreamDestroy(ln.stream2);
+        if (ln.ev_fork) hipEventDestroy(ln.ev_fork);
+        if (ln.ev_join) hipEventDestroy(ln.ev_join);
+        if (ln.ev_free) hipEventDestroy(ln.ev_free);
+        if (ln.stream) hipStreamDestroy(ln.stream);
     }
-    if (R.ev_fork) hipEventDestroy(R.ev_fork);
-    if (R.ev_join) hipEventDestroy(R.ev_join);
-    if (R.ev_free) hipEventDestroy(R.ev_free);
-    if (R.stream) hipStreamDestroy(R.stream);
+    R.lanes.clear();
+    for (void *p : R.weight_allocs) hipFree(p);
 }
 
 std::vector<int> parse_device_env(int n_visible) {
@@ -1263,6 +1292,8 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     f6_select(ctx.get());
     if (const char *e = std::getenv("BERT_AMD_SPLIT")) ctx->split = e[0] != '0';
     if (const char *e = std::getenv("BERT_AMD_PACK")) ctx->pack = e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
+    if (const char *e = std::getenv("BERT_AMD_FUSE_MIN")) ctx->fuse_min = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("BERT_AMD_ENCODE_LANES")) ctx->encode_lanes = std::max(1, std::atoi(e));
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {
@@ -1318,15 +1349,15 @@ bool grow_pinned(Workspace &w, int64_t rows, int64_t seqs, int64_t E) {
 
 // Evaluate sentences [s0, s1) of a host batch on replica R; results go
 // straight into the caller's embedding rows.
-bool eval_host_slice(bert_ctx *ctx, Replica &R, bert_vocab_id **toks, const int32_t *ntok, float **embs, int s0,
+bool eval_host_slice(bert_ctx *ctx, Replica &R, Lane &ln, bert_vocab_id **toks, const int32_t *ntok, float **embs, int s0,
                      int s1) {
     const int n = s1 - s0;
     if (n <= 0) return true;
     HIP_OK(hipSetDevice(R.device));
     int64_t M = 0;
     for (int s = s0; s < s1; s++) M += ntok[s];
-    if (!grow_pinned(R.ws, M, n, ctx->hp.n_embd)) return false;
-    Workspace &w = R.ws;
+    if (!grow_pinned(ln.ws, M, n, ctx->hp.n_embd)) return false;
+    Workspace &w = ln.ws;
     // token rows contiguous in the caller's memory (one [n][len] array): upload
     // them from there instead of gathering them into the pinned buffer first
     bool tok_direct = true;
@@ -1340,12 +1371,12 @@ bool eval_host_slice(bert_ctx *ctx, Replica &R, bert_vocab_id **toks, const int3
     if (!tok_direct)
         for (int s = s0; s < s1; s++) std::memcpy(w.h_tok + w.h_off[s - s0], toks[s], (size_t)ntok[s] * 4);
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
-    const hipStream_t st = R.stream;
-    if (!ensure_workspace(ctx, R, Mpad, n, st) || !ws_acquire(R, st)) return false;
+    const hipStream_t st = ln.stream;
+    if (!ensure_workspace(ctx, ln, Mpad, n, st) || !ws_acquire(ln, st)) return false;
     HIP_OK(hipMemcpyAsync(w.tok, tok_direct ? toks[s0] : w.h_tok, (size_t)M * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(w.off, w.h_off, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
-    const bool ok = run_pipeline(ctx, R, w.tok, w.off, w.h_off, n, w.out, st);
-    if (!ws_release(R, st) || !ok) return false;
+    const bool ok = run_pipeline(ctx, R, ln, w.tok, w.off, w.h_off, n, w.out, st);
+    if (!ws_release(ln, st) || !ok) return false;
     const int E = ctx->hp.n_embd;
     // caller rows contiguous (one [n][E] array, the usual case): the embeddings
     // go straight from the device into them, without the pinned bounce buffer
@@ -1409,6 +1440,77 @@ int greedy_tiles(const int32_t *ntok, const std::vector<int> &order) {
     return tiles;
 }
 
+// A batch whose sentences all fit one 128-row tile runs the fused QKV +
+// attention kernel; a mixed batch is evaluated as two ragged batches (short
+// sentences, then the rest), so one long sentence does not move every short
+// one onto the unfused pair.  Sentences are independent, so the results do
+// not depend on the grouping.  The short sentences are also put in tile order
+// (tile_order) so that they share fused-kernel workgroups.  `run` evaluates
+// one group.
+template <typename F>
+void eval_grouped(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs, F run) {
+    const HParams &hp = ctx->hp;
+    if (!qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, GEMM_BM)) {
+        run(n, toks, ntok, embs);
+        return;
+    }
+    std::vector<int> shrt, lng;
+    for (int s = 0; s < n; s++) (ntok[s] <= GEMM_BM ? shrt : lng).push_back(s);
+    shrt = tile_order(ntok, shrt);
+    for (const std::vector<int> *grp : {&shrt, &lng}) {
+        if (grp->empty()) continue;
+        std::vector<bert_vocab_id *> t;
+        std::vector<int32_t> c;
+        std::vector<float *> e;
+        for (int s : *grp) {
+            t.push_back(toks[s]);
+            c.push_back(ntok[s]);
+            e.push_back(embs[s]);
+        }
+        run((int32_t)grp->size(), t.data(), c.data(), e.data());
+    }
+}
+
+// bert_encode_batch's slices [k * chunk, ...) of the length-sorted inputs,
+// several at once: every replica gets ctx->encode_lanes lanes (created on
+// first use), each lane a host thread that takes the next slice and evaluates
+// it on its own workspace and streams — small slices (the reference consumers
+// pass 16) each fill only a few CUs, so running them side by side is what
+// fills the device.  Each slice is still one ragged batch of at most chunk
+// sentences, evaluated exactly as bert_eval_batch would (results identical).
+void encode_slices(bert_ctx *ctx, int32_t n, int32_t chunk, bert_vocab_id **toks, int32_t *ntok, float **embs) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const int nslice = (n + chunk - 1) / chunk, nr = (int)ctx->reps.size();
+    const int nl = std::max(1, std::min(ctx->encode_lanes, (nslice + nr - 1) / nr));
+    for (auto &r : ctx->reps) {
+        if ((int)r->lanes.size() >= nl) continue;
+        if (hipSetDevice(r->device) != hipSuccess) return;
+        while ((int)r->lanes.size() < nl)
+            if (!add_lane(*r)) {
+                std::fprintf(stderr, "bert_encode_batch: %s\n", g_err.c_str());
+                return;
+            }
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < nr; r++)
+        for (int l = 0; l < nl; l++)
+            th.emplace_back([&, r, l] {
+                Replica &R = *ctx->reps[r];
+                Lane &ln = *R.lanes[l];
+                for (int k = next++; k < nslice; k = next++) {
+                    const int32_t s0 = k * chunk, m = std::min(chunk, n - s0);
+                    eval_grouped(ctx, m, toks + s0, ntok + s0, embs + s0,
+                                 [&](int32_t mm, bert_vocab_id **t, int32_t *c, float **e) {
+                                     if (!eval_host_slice(ctx, R, ln, t, c, e, 0, mm))
+                                         std::fprintf(stderr, "bert_encode_batch: device %d: %s\n", R.device,
+                                                      g_err.c_str());
+                                 });
+                }
+            });
+    for (auto &t : th) t.join();
+}
+
 // Host-pointer batch eval, sharded over the context's replicas by token count.
 void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
     if (!ctx || n <= 0 || !toks || !ntok || !embs) return;
@@ -1428,33 +1530,9 @@ void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *nt
             }
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
-    // A batch whose sentences all fit one 128-row tile runs the fused QKV +
-    // attention kernel; a mixed batch is evaluated as two ragged batches
-    // (short sentences, then the rest), so one long sentence does not move
-    // every short one onto the unfused pair.  Sentences are independent, so
-    // the results do not depend on the grouping.
-    // The short sentences are also put in tile order (tile_order) so that they
-    // share fused-kernel workgroups.
-    const HParams &hp = ctx->hp;
-    if (qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, GEMM_BM)) {
-        std::vector<int> shrt, lng;
-        for (int s = 0; s < n; s++) (ntok[s] <= GEMM_BM ? shrt : lng).push_back(s);
-        shrt = tile_order(ntok, shrt);
-        for (const std::vector<int> *grp : {&shrt, &lng}) {
-            if (grp->empty()) continue;
-            std::vector<bert_vocab_id *> t;
-            std::vector<int32_t> c;
-            std::vector<float *> e;
-            for (int s : *grp) {
-                t.push_back(toks[s]);
-                c.push_back(ntok[s]);
-                e.push_back(embs[s]);
-            }
-            dispatch_batch(ctx, (int32_t)grp->size(), t.data(), c.data(), e.data());
-        }
-        return;
-    }
-    dispatch_batch(ctx, n, toks, ntok, embs);
+    eval_grouped(ctx, n, toks, ntok, embs, [&](int32_t m, bert_vocab_id **t, int32_t *c, float **e) {
+        dispatch_batch(ctx, m, t, c, e);
+    });
 }
 
 // Shards one ragged batch over the context's replicas (caller holds ctx->mu).
@@ -1475,7 +1553,7 @@ void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *nto
         for (; r < nr; r++) cut[r] = n;
     }
     if (nr == 1) {
-        if (!eval_host_slice(ctx, *ctx->reps[0], toks, ntok, embs, 0, n))
+        if (!eval_host_slice(ctx, *ctx->reps[0], *ctx->reps[0]->lanes[0], toks, ntok, embs, 0, n))
             std::fprintf(stderr, "bert_eval_batch: %s\n", g_err.c_str());
         return;
     }
@@ -1483,7 +1561,8 @@ void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *nto
     std::vector<std::string> errs(nr);
     for (int r = 0; r < nr; r++)
         th.emplace_back([&, r] {
-            if (!eval_host_slice(ctx, *ctx->reps[r], toks, ntok, embs, cut[r], cut[r + 1])) errs[r] = g_err;
+            if (!eval_host_slice(ctx, *ctx->reps[r], *ctx->reps[r]->lanes[0], toks, ntok, embs, cut[r], cut[r + 1]))
+                errs[r] = g_err;
         });
     for (auto &t : th) t.join();
     for (int r = 0; r < nr; r++)
@@ -1597,20 +1676,34 @@ void bert_encode_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, i
     // reference bert.cpp:1119-1198: tokenise everything, sort by token count
     // (std::sort on the lengths, :1176-1177), evaluate in slices of
     // n_batch_size (the reference forces the slice to 1, :1128; here each
-    // slice is one ragged GPU batch).  n_batch_size bounds the per-call
-    // working set (device workspace and pinned staging grow to the largest
-    // slice); n_batch_size <= 0 means all inputs in one slice.  Sorting makes
-    // each slice's lengths similar, so padding and tile waste stay small.
+    // slice is one ragged GPU batch, and up to encode_lanes slices per device
+    // run at once: encode_slices).  n_batch_size bounds each slice's working
+    // set (a lane's device workspace and pinned staging grow to the largest
+    // slice it ran); n_batch_size <= 0 means all inputs in one slice.  Sorting
+    // makes each slice's lengths similar, so padding and tile waste stay small.
     if (!ctx || n_inputs <= 0 || !texts || !embeddings) return;
     const int32_t N = ctx->hp.n_max_tokens;
     std::vector<bert_vocab_id> buf((size_t)N * n_inputs);
     std::vector<int32_t> ntok(n_inputs);
     std::vector<bert_vocab_id *> ptr(n_inputs);
-    bert_vocab_id *ids = buf.data();
-    for (int i = 0; i < n_inputs; i++) {
-        ptr[i] = ids;
-        bert_tokenize(ctx, texts[i], ids, &ntok[i], N);
-        ids += ntok[i];
+    // tokenisation on n_threads host threads (the reference's thread count;
+    // its CPU graph used them, bert.cpp:1128): contiguous ranges of inputs,
+    // each into its own N-token slots of `buf` (the tokenizer is stateless)
+    const int nt = std::max(1, std::min({(int)n_threads, n_inputs / 64 + 1,
+                                         (int)std::max(1u, std::thread::hardware_concurrency())}));
+    auto tok_range = [&](int a, int b) {
+        for (int i = a; i < b; i++) {
+            ptr[i] = buf.data() + (size_t)i * N;
+            bert_tokenize(ctx, texts[i], ptr[i], &ntok[i], N);
+        }
+    };
+    if (nt == 1) {
+        tok_range(0, n_inputs);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; t++)
+            th.emplace_back(tok_range, (int)((int64_t)n_inputs * t / nt), (int)((int64_t)n_inputs * (t + 1) / nt));
+        for (auto &t : th) t.join();
     }
     std::vector<int> idx(n_inputs);
     for (int i = 0; i < n_inputs; i++) idx[i] = i;
@@ -1624,9 +1717,14 @@ void bert_encode_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, i
         se[i] = embeddings[idx[i]];
     }
     const int32_t chunk = n_batch_size > 0 ? std::min(n_batch_size, n_inputs) : n_inputs;
-    for (int32_t i = 0; i < n_inputs; i += chunk) {
-        const int32_t m = std::min(chunk, n_inputs - i);
-        bert_eval_batch(ctx, n_threads, m, sp.data() + i, sn.data() + i, se.data() + i);
+    if (chunk >= n_inputs) {
+        bert_eval_batch(ctx, n_threads, n_inputs, sp.data(), sn.data(), se.data());
+        return;
+    }
+    try {
+        encode_slices(ctx, n_inputs, chunk, sp.data(), sn.data(), se.data());
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "bert_encode_batch: %s\n", e.what());
     }
 }
 
@@ -1681,13 +1779,14 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
     // the caller's stream, as given: NULL is HIP's null (legacy default)
     // stream, which is ordered with the caller's other work on it
     const hipStream_t st = (hipStream_t)hip_stream;
-    if (!ws_acquire(R, st)) return -3;
+    Lane &ln = *R.lanes[0];
+    if (!ws_acquire(ln, st)) return -3;
     // every return below the acquire records the hand-over event first
     struct Release {
-        Replica &R;
+        Lane &ln;
         hipStream_t st;
-        ~Release() { ws_release(R, st); }
-    } release{R, st};
+        ~Release() { ws_release(ln, st); }
+    } release{ln, st};
     try {
         // Short sentences in the caller's order may leave fused-kernel tiles
         // half empty: when the tile order (tile_order) needs fewer workgroups,
@@ -1705,8 +1804,8 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
             if (t_order < greedy_tiles(ntok.data(), idx) && qkv_attention_pack_pays(n_seqs, t_order)) {
                 const int64_t M = h_offsets[n_seqs];
                 const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
-                if (!ensure_workspace(ctx, R, Mpad, n_seqs, st)) return -4;
-                Workspace &w = R.ws;
+                if (!ensure_workspace(ctx, ln, Mpad, n_seqs, st)) return -4;
+                Workspace &w = ln.ws;
                 std::vector<int32_t> off2(n_seqs + 1), perm(order.begin(), order.end());
                 off2[0] = 0;
                 for (int i = 0; i < n_seqs; i++) off2[i + 1] = off2[i] + ntok[order[i]];
@@ -1717,11 +1816,11 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
                     set_err("bert_amd_eval_device: reorder failed");
                     return -4;
                 }
-                if (!run_pipeline(ctx, R, w.tok, w.off, off2.data(), n_seqs, d_out, st, w.perm)) return -4;
+                if (!run_pipeline(ctx, R, ln, w.tok, w.off, off2.data(), n_seqs, d_out, st, w.perm)) return -4;
                 return 0;
             }
         }
-        if (!run_pipeline(ctx, R, d_tokens, d_offsets, h_offsets, n_seqs, d_out, st)) return -4;
+        if (!run_pipeline(ctx, R, ln, d_tokens, d_offsets, h_offsets, n_seqs, d_out, st)) return -4;
     } catch (const std::exception &e) {
         set_err("%s", e.what());
         return -5;
@@ -1792,13 +1891,14 @@ int32_t bert_amd_debug_embed(bert_ctx *ctx, const int32_t *tokens, const int32_t
     try {
         Replica &R = *ctx->reps[0];
         HIP_OK_RC(hipSetDevice(R.device), -3);
-        const hipStream_t st = R.stream;
+        Lane &ln = *R.lanes[0];
+        const hipStream_t st = ln.stream;
         const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
-        if (!ensure_workspace(ctx, R, Mpad, n_seqs, st) || !ws_acquire(R, st)) return -3;
-        Workspace &w = R.ws;
+        if (!ensure_workspace(ctx, ln, Mpad, n_seqs, st) || !ws_acquire(ln, st)) return -3;
+        Workspace &w = ln.ws;
         HIP_OK_RC(hipMemcpyAsync(w.tok, tokens, (size_t)M * 4, hipMemcpyHostToDevice, st), -3);
         HIP_OK_RC(hipMemcpyAsync(w.off, offsets, (size_t)(n_seqs + 1) * 4, hipMemcpyHostToDevice, st), -3);
-        const EmbedArgs ea = embed_args(ctx, R, w.tok, w.off, n_seqs, M);
+        const EmbedArgs ea = embed_args(ctx, R, w, w.tok, w.off, n_seqs, M);
         HIP_OK_RC(launch_embed(ctx->wtype, ea, (int)Mpad, st), -4);
         const int64_t E = ctx->hp.n_embd;
         HIP_OK_RC(hipMemcpyAsync(X_out, w.X, (size_t)(M * E) * 4, hipMemcpyDeviceToHost, st), -3);
@@ -1806,7 +1906,7 @@ int32_t bert_amd_debug_embed(bert_ctx *ctx, const int32_t *tokens, const int32_t
         if (d_out && act_scale_bytes(ctx->wtype))
             HIP_OK_RC(hipMemcpyAsync(d_out, w.Xa.d, (size_t)(M * (E / 32)) * act_scale_bytes(ctx->wtype),
                                      hipMemcpyDeviceToHost, st), -3);
-        ws_release(R, st);
+        ws_release(ln, st);
         HIP_OK_RC(hipStreamSynchronize(st), -3);
     } catch (const std::exception &e) {
         set_err("%s", e.what());
@@ -1830,6 +1930,18 @@ int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
             return -2;
         }
         ctx->pack = value;
+    } else if (k == "encode_lanes") {
+        if (value < 1) {
+            set_err("bert_amd_set_option: encode_lanes must be >= 1");
+            return -2;
+        }
+        ctx->encode_lanes = value;
+    } else if (k == "fuse_min") {
+        if (value < 0) {
+            set_err("bert_amd_set_option: fuse_min must be >= 0");
+            return -2;
+        }
+        ctx->fuse_min = value;
     } else {
         set_err("bert_amd_set_option: unknown option '%s'", key);
         return -2;
@@ -1840,7 +1952,9 @@ int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
 int64_t bert_amd_workspace_rows(bert_ctx *ctx, int32_t slot) {
     if (!ctx || slot < 0 || slot >= (int32_t)ctx->reps.size()) return -1;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    return ctx->reps[slot]->ws.cap_rows;
+    int64_t rows = 0;  // the largest lane (bert_encode_batch may have added lanes)
+    for (auto &ln : ctx->reps[slot]->lanes) rows = std::max(rows, ln->ws.cap_rows);
+    return rows;
 }
 
 const char *bert_amd_last_error(void) { return g_err.c_str(); }

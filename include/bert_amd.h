@@ -88,10 +88,18 @@ BERT_API int32_t bert_amd_debug_embed(struct bert_ctx *ctx, const int32_t *token
 BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
 
 /* Per-context pipeline options (read from the environment once at load,
-   BERT_AMD_SPLIT / BERT_AMD_PACK; this call changes them afterwards):
+   BERT_AMD_SPLIT / BERT_AMD_PACK / BERT_AMD_FUSE_MIN / BERT_AMD_ENCODE_LANES;
+   this call changes them
+   afterwards):
      "split" 0 | 1     run large fused batches as two row groups on two streams
      "pack"  -1 | 0 | 1 pack short sentences into shared fused-kernel tiles
                         when it pays (-1, default) / never / always
+     "fuse_min" n >= 0 batches of fewer than n sentences (default 48) run the
+                        unfused QKV GEMM + attention pair instead of the fused
+                        kernel (lower latency for small batches)
+     "encode_lanes" n >= 1 bert_encode_batch slices evaluated at once per
+                        device (default 4; BERT_AMD_ENCODE_LANES), each on its
+                        own workspace bounded by n_batch_size
    Results are identical under every setting. */
 BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int32_t value);
 

@@ -64,13 +64,17 @@ def test_golden_vectors(case, model_dir):
 
 def parity_bound(meta):
     """Per-sentence bound on 1 - cos vs the AVX2 oracle: the north star's
-    1e-4 (cos >= 0.9999), or — where ggml's OWN builds land further apart on
-    that input — twice the measured spread between ggml@8ca2c19's summation
-    orders (fixture field ggml_order_spread_1mcos: plain-C and 16-lane builds
-    vs the AVX2 build, tests/golden/make_golden.py order_spread).  Only the
-    24-layer bge Q4_1 fixture (spread 1.8e-3 / 2.3e-3) and the sigma = 0.1
-    stress model (9.3e-5) come near or past 1e-4."""
-    return np.maximum(1 - COS_TOL, 2.0 * np.asarray(meta["ggml_order_spread_1mcos"]))
+    1e-4 (cos >= 0.9999), or — where ggml's own builds land further apart on
+    that input — the spread between the oracle's restatements of ggml@8ca2c19's
+    summation orders (fixture field ggml_order_spread_1mcos: plain-C and
+    16-lane variants vs the AVX2 one, tests/golden/make_golden.py
+    order_spread), with no widening factor.  PARITY UNPINNED: those variants
+    are restatements, not ggml builds (ggml is absent from the reference), so
+    whether they reproduce ggml's own builds is not verified.
+    Only the 24-layer bge Q4_1 fixture (spread 1.8e-3 / 2.3e-3; the GPU lands
+    at 1.50e-3 / 1.75e-3) and the sigma = 0.1 stress model (9.3e-5; GPU 9.8e-5
+    under the 1e-4 floor) come near or past 1e-4."""
+    return np.maximum(1 - COS_TOL, np.asarray(meta["ggml_order_spread_1mcos"]))
 
 
 @pytest.mark.xfail(strict=True, reason="ggml's own builds differ by 1-cos 1.8e-3 / 2.3e-3 on these inputs "
@@ -619,3 +623,62 @@ def test_eval_batch_strided_rows_match_contiguous(model_dir):
     m.lib.bert_eval_batch(m.ctx, 1, n, tok_p, ntok, out_p)
     assert np.array_equal(big_e[::2], ref)
     assert np.all(np.isnan(big_e[1::2]))  # rows between the caller's rows untouched
+
+
+def test_default_load_spans_visible_devices(model_dir):
+    """bert_load_from_file shards over every visible device (BERT_AMD_DEVICES
+    unset): bert_amd_n_devices equals the device count, and with more than one
+    physical device the sharded batch is bitwise one replica's."""
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    hip = Hip()
+    n = hip.c.c_int(0)
+    hip.check(hip.L.hipGetDeviceCount(hip.c.byref(n)))
+    mall = bertlib.BertModel(p)  # the reference entry point
+    try:
+        assert mall.n_devices == n.value
+        if n.value > 1:
+            toks = [sentence(50 + i, ln, 30522) for i, ln in enumerate([128, 9, 256, 64, 2, 500, 128, 77] * 8)]
+            m0 = bertlib.BertModel(p, devices=[0])
+            try:
+                assert np.array_equal(mall.eval_batch(toks), m0.eval_batch(toks))
+            finally:
+                m0.close()
+    finally:
+        mall.close()
+
+
+@pytest.mark.parametrize("shape,ftype", [("minilm", "q4_0"), ("minilm", "f16")])
+def test_small_batches_unfused_bitwise_fused(shape, ftype, model_dir):
+    """Batches under fuse_min sentences run the unfused QKV GEMM + attention
+    pair (latency: one fused workgroup per sentence bounds a small batch);
+    every sentence's embedding is bitwise the fused kernel's, so a sentence's
+    result does not depend on the size of the batch it came in."""
+    p, m = get_model(model_dir, shape, ftype)
+    toks = [sentence(700 + i, n, 30522) for i, n in enumerate([128, 3, 64, 100, 31, 32, 33, 127] * 8)]
+    try:
+        m.set_option("fuse_min", 0)
+        fused = m.eval_batch(toks)
+        m.set_option("fuse_min", 10 ** 6)
+        unfused = m.eval_batch(toks)
+    finally:
+        m.set_option("fuse_min", 48)
+    assert np.array_equal(fused, unfused)
+    assert np.array_equal(m.eval(toks[5]), fused[5])
+
+
+def test_encode_batch_lanes_bitwise(model_dir):
+    """bert_encode_batch with many small slices runs them on several lanes
+    (workspaces + streams) at once; every embedding equals the one-batch
+    result bitwise, whatever the lane count."""
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    m = bertlib.BertModel(p)
+    try:
+        rng = np.random.default_rng(11)
+        texts = [" ".join(f"w{int(x)}" for x in rng.integers(0, 500, int(k))) for k in rng.integers(1, 120, 300)]
+        want = m.eval_batch([m.tokenize(t) for t in texts])
+        for lanes in (1, 4, 7):
+            m.set_option("encode_lanes", lanes)
+            assert np.array_equal(m.encode(texts, batch_size=16), want)
+        assert np.array_equal(m.encode(texts, batch_size=256), want)
+    finally:
+        m.close()
