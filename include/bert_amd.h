@@ -97,9 +97,14 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
      "fuse_min" n >= 0 batches of fewer than n sentences (default 48) run the
                         unfused QKV GEMM + attention pair instead of the fused
                         kernel (lower latency for small batches)
-     "encode_lanes" n >= 1 bert_encode_batch slices evaluated at once per
-                        device (default 4; BERT_AMD_ENCODE_LANES), each on its
-                        own workspace bounded by n_batch_size
+     "encode_lanes" n >= 1 bert_encode_batch: lanes per device, each a host
+                        thread with its own workspace and streams (default 2;
+                        BERT_AMD_ENCODE_LANES)
+     "encode_merge" n >= 1 bert_encode_batch: consecutive n_batch_size slices a
+                        lane evaluates as one ragged batch (default 4;
+                        BERT_AMD_ENCODE_MERGE; 1 = one slice per GPU batch).
+                        At most lanes x merge x n_batch_size sentences are in
+                        flight per device
    Results are identical under every setting. */
 BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int32_t value);
 

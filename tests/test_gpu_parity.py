@@ -375,6 +375,7 @@ def test_encode_batch_slices_sorted_and_bounded(model_dir):
         rng = np.random.default_rng(7)
         texts = [" ".join(f"w{int(x)}" for x in rng.integers(0, 500, int(k))) for k in rng.integers(1, 60, 40)]
         ids = [m.tokenize(t) for t in texts]
+        m.set_option("encode_merge", 1)  # one n_batch_size slice per GPU batch
         emb = m.encode(texts, batch_size=8)
         longest8 = sum(sorted(len(i) for i in ids)[-8:])
         assert 0 < m.workspace_rows() <= (longest8 + 127) // 128 * 128
@@ -676,8 +677,9 @@ def test_encode_batch_lanes_bitwise(model_dir):
         rng = np.random.default_rng(11)
         texts = [" ".join(f"w{int(x)}" for x in rng.integers(0, 500, int(k))) for k in rng.integers(1, 120, 300)]
         want = m.eval_batch([m.tokenize(t) for t in texts])
-        for lanes in (1, 4, 7):
+        for lanes, merge in ((1, 1), (4, 1), (7, 1), (2, 4), (3, 5)):
             m.set_option("encode_lanes", lanes)
+            m.set_option("encode_merge", merge)
             assert np.array_equal(m.encode(texts, batch_size=16), want)
         assert np.array_equal(m.encode(texts, batch_size=256), want)
     finally:
