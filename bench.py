@@ -326,6 +326,7 @@ def main():
     dominant = max(prof, key=lambda k: prof[k][0]) if prof else None
 
     roofline = None
+    hbm_step = None
     if dominant:
         avg_s = prof[dominant][0] / prof[dominant][1] / 1e3
         fl = kernel_flops(dominant, B, N, hp)
@@ -356,6 +357,18 @@ def main():
                     tsrc = f"profiles/pmc_traffic.json ({pt.get('source', '')})"
         roofline["traffic"] = traffic
         roofline["traffic_source"] = tsrc
+        # whole-step achieved HBM (north_star): PMC bytes of one step's launches
+        # (profiles/pmc_traffic.json bytes_per_step) over this run's ms_per_step
+        pf = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(pf):
+            with open(pf) as f:
+                pt = json.load(f)
+            if pt.get("workload") == f"{args.shape} {args.ftype} batch={B} seq_len={N}" and pt.get("bytes_per_step"):
+                bps = float(pt["bytes_per_step"])
+                gbs = bps / (ms_per_step * 1e-3) / 1e9
+                hbm_step = dict(bytes_per_step=round(bps), achieved_GBs=round(gbs, 1), peak_GBs=PEAK_HBM_GBS,
+                                frac=round(gbs / PEAK_HBM_GBS, 4),
+                                source=f"profiles/pmc_traffic.json ({pt.get('source', '')}) over this run's ms_per_step")
         roofline["algorithmic_bytes_per_launch"] = kernel_bytes(dominant, B, N, hp, args.ftype)
 
     # whole-path MFMA fraction: F(N) = L(8NE^2 + 4NEI + 4N^2E) per sentence
@@ -530,6 +543,7 @@ def main():
                        "global_batch": B * world, "seq_len": N, "parallelism": f"dp{world}"},
             "roofline": roofline,
             "pipeline_mfma_frac": round(path_frac, 4),
+            "step_hbm": hbm_step,
             "kernels": kern,
             "kernels_note": "per-kernel HIP-event pass with one row group (bert_amd_set_option split 0); the timed steps "
                             "run two row groups on two streams (runtime.cpp run_pipeline)",

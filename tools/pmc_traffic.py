@@ -44,6 +44,10 @@ def main():
             out["fetch_bytes"][name] = round(fb)
             out["write_bytes"][name] = round(wb)
             out["bytes_per_launch"][name] = round(fb + wb)
+    # whole step: every layer kernel launches n_layer (6) times per step, embed and pool once
+    per_step = {"embed_ln": 1, "pool_l2": 1}
+    if all(k in out["bytes_per_launch"] for k in NAMES):
+        out["bytes_per_step"] = round(sum(b * per_step.get(k, 6) for k, b in out["bytes_per_launch"].items()))
     with open(sys.argv[4], "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["bytes_per_launch"]))
