@@ -440,12 +440,22 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
 // w (32 features) of both 32-token t-tiles, so a row's 384 values are spread
 // over 12 waves x 2 lane halves x 16.  ggml_norm's double sums go lane ->
 // lane pair -> the twelve waves (LDS partials, fixed order).
+// The residual tile (64 rows x 384 f32, 96 KiB, contiguous in X) moves between
+// HBM and the workgroup through LDS in whole 1 KiB pieces: in by LDS-DMA
+// (global_load_lds_dwordx4, 8 per wave), out by 16-byte stores of consecutive
+// threads — instead of each lane gathering and scattering its own row (32
+// cache lines per wave instruction).  16-byte chunk c of row r sits at LDS
+// chunk c ^ (r & 15), so the epilogue's row-per-lane reads are conflict-free.
+__device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ (r & 15)); }
+
 template <int WT>
 __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles) {
     constexpr int NT = 768, BM = 64, F = 1, T = 2, NCOL = 384, NWV = 12;
+    constexpr int XCH = BM * NCOL / 4;  // 16-byte chunks of the residual tile
     using C = I8Chunk<BM, WT == W_Q4_1>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ double red[2][NWV][BM];
+    __shared__ __attribute__((aligned(16))) float xs[BM * NCOL];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int ft0 = wv;
     const int col = 32 * ft0 + 16 * hh;
@@ -458,15 +468,25 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
         if (tile + (int)gridDim.x < n_mtiles) m0n = (int64_t)xcd_linear(tile + gridDim.x, n_mtiles) * BM;
         float16v acc[F][T];
         i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc);
+        {   // residual tile -> xs: wave w's LDS-DMA k covers LDS chunks 64 (8 w + k) ..
+            const float *xt = g.X + m0 * NCOL;
+#pragma unroll 1
+            for (int k = 0; k < XCH / NT; k++) {
+                const int j0 = 64 * (8 * wv + k), j = j0 + lane, r = j / 96, cs = j - 96 * r;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(xt + r * NCOL + 4 * (cs ^ (r & 15))),
+                    (__attribute__((address_space(3))) void *)(xs + 4 * j0), 16, 0, 0);
+            }
+        }
+        __syncthreads();  // (drains the LDS-DMA: vmcnt(0) before the barrier)
         // v = (b + W.x) + x  (ggml: add(repeat(b), mul_mat) then add(cur, inpL))
 #pragma unroll
         for (int t = 0; t < T; t++) {
             const int r = 32 * t + l32;
-            const float4v *xp = (const float4v *)(g.X + (m0 + r) * NCOL + col);
             double s = 0.0;
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
-                const float4v x4 = xp[qq];
+                const float4v x4 = *(const float4v *)(xs + 4 * i8_xs_chunk(r, (col >> 2) + qq));
                 const float4v b4 = *(const float4v *)(g.bias + col + 4 * qq);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -518,11 +538,23 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
                     z = w4[j] * z;
                     y[4 * qq + j] = z + b4[j];
                 }
-                *(float4v *)(g.X + row * NCOL + col + 4 * qq) = float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
+                // in place: each (row, chunk) is this lane's alone
+                *(float4v *)(xs + 4 * i8_xs_chunk(r, (col >> 2) + qq)) =
+                    float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
             }
             i8_store_q8_half<WT>(g.out_act, NCOL, row, ft0, hh, y);
         }
-        // the next tile's main loop reuses `red` only after its own barriers
+        __syncthreads();
+        {   // xs -> X: consecutive threads store consecutive 16-byte chunks
+            float *xt = g.X + m0 * NCOL;
+#pragma unroll 1
+            for (int k = 0; k < XCH / NT; k++) {
+                const int j = tid + NT * k, r = j / 96, cs = j - 96 * r;
+                *(float4v *)(xt + r * NCOL + 4 * (cs ^ (r & 15))) = *(const float4v *)(xs + 4 * j);
+            }
+        }
+        // the next tile's main loop reuses `red` and its LDS-DMA rewrites xs only
+        // after the main loop's own barriers
     }
 }
 
