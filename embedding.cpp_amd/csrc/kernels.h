@@ -28,7 +28,10 @@ namespace bertamd {
 // W_Q4_0D: Q4_0 weights whose GEMMs run on the block-scaled fp6 MFMA
 // (gemm_f6.hip); the same ggml Q8_0 activations (d, q), stored as Q8D: per
 // 32-block 48 bytes of fp6 digit codes (kernels_common.h q8d_*) + fp16 d.
-enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3, W_Q4_0D = 4 };
+enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3, W_Q4_0D = 4, W_Q4_0N = 5 };
+// W_Q4_0N: Q4_0 weights kept as ggml's nibbles and dequantised inside the fp16
+// MFMA GEMM (WPtr below); its activations are Q4_0's (ggml Q8_0).
+constexpr int act_of(int wt) { return wt == W_Q4_0N ? W_Q4_0 : wt; }
 constexpr int Q8D_BLK = 48;  // code bytes per Q8D block
 
 struct ActPtr {
@@ -47,11 +50,18 @@ struct ActPtr {
 //         lo = fp16(w - hi).  For Q4_0 the split is exact (w has <= 15
 //         significant bits), so an fp16 MFMA over integer Q8 activations
 //         returns d_w * sum(q_a * q_w) exactly in each product; `unscale` = 2^-S.
+//   Q4_0N: q = uint32 [N/16][K/32][64]: lane (c, g)'s 8 nibbles q (k = 8 g + j
+//         at bits 4 (j >> 1) + 16 (j & 1), so one and-or per pair makes two
+//         fp16 integers 1024 + q); d = fp16 [N/16][K/32][16] (d_w of column c).
+//         The MFMA takes q - 8 as exact fp16 integers against the Q8 codes
+//         (isum exact in f32) and the fold applies d_w * d_a per block, as
+//         ggml_vec_dot_q4_0_q8_0; 0.56 B per weight.
 //   F16 : q = fp16 [N/16][K/32][64][8]
 //   F32 : q = f32  [N/16][K/32][64][8]
 struct WPtr {
     const void *q = nullptr;
     float unscale = 1.f;
+    const uint16_t *d = nullptr;  // Q4_0N block scales
 };
 
 // Q4_0 / Q4_1 weights for the int8-MFMA GEMMs (gemm_i8.hip), repacked at load

@@ -451,6 +451,9 @@ __device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item,
 
 template <int WT> struct WFrag;
 template <> struct WFrag<W_Q4_0> { half8 hi, lo; };
+// Q4_0N: one 16-byte record per lane: 8 nibbles, the fp16 d_w of columns
+// 4g .. 4g + 3 (transposed main loop) and of column c16 (plain)
+template <> struct WFrag<W_Q4_0N> { u32x4v r; };
 template <> struct WFrag<W_Q4_1> { half8 hi, lo; };
 template <> struct WFrag<W_F16> { half8 h; };
 template <> struct WFrag<W_F32> { float4v f[2]; };
@@ -459,7 +462,9 @@ template <int WT>
 __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
     const int lane = threadIdx.x & 63;
     WFrag<WT> f;
-    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+    if constexpr (WT == W_Q4_0N) {
+        f.r = ((const u32x4v *)W.q)[tile * 64 + lane];
+    } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         f.hi = ((const half8 *)W.q)[(tile * 2) * 64 + lane];
         f.lo = ((const half8 *)W.q)[(tile * 2 + 1) * 64 + lane];
     } else if constexpr (WT == W_F16) {
@@ -469,6 +474,20 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
         f.f[1] = ((const float4v *)W.q)[(tile * 64 + lane) * 2 + 1];
     }
     return f;
+}
+
+// Q4_0N: 8 nibbles (k = 2 s + e at bits 4 s + 16 e) -> q - 8 as exact fp16
+// integers: (0x6400 | q) is 1024 + q, one and-or and one packed subtract per pair
+__device__ __forceinline__ half8 nib_to_f16(uint32_t x) {
+    const half2v off = {(_Float16)1032.f, (_Float16)1032.f};
+    half8 w;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const half2v h = __builtin_bit_cast(half2v, ((x >> (4 * s)) & 0x000f000fu) | 0x64006400u) - off;
+        w[2 * s] = h[0];
+        w[2 * s + 1] = h[1];
+    }
+    return w;
 }
 
 // GEMM main loop, shared by gemm_kernel and qkv_attention_kernel:
@@ -484,7 +503,7 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
 template <int WT, int NW, int BM, int NTW>
 struct MainloopPre {
     static constexpr int IT = (BM * (KC / 16) + NW * 64 - 1) / (NW * 64);
-    AReg<WT> ar[IT];
+    AReg<act_of(WT)> ar[IT];
     WFrag<WT> wf[WT == W_F32 ? 1 : 2][NTW];
 };
 
@@ -501,7 +520,7 @@ __device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW> &p
         // scratch 64 -> 20 bytes per lane)
         int item = tid + it * NT;
         asm volatile("" : "+v"(item));
-        if (item < ITEMS) a_load<WT>(pre.ar[it], args.A, args.K, m0, 0, item);
+        if (item < ITEMS) a_load<act_of(WT)>(pre.ar[it], args.A, args.K, m0, 0, item);
     }
     if constexpr (WT != W_F32) {
 #pragma unroll
@@ -517,7 +536,8 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     static_assert(!TRANS || WT != W_F32, "transposed main loop: fp16 MFMA formats only");
     constexpr int NT = NW * 64;
     constexpr int RT = BM / 16;
-    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr bool QN = WT == W_Q4_0N, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
+    constexpr int AT = act_of(WT);
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
     constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
@@ -532,12 +552,12 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
 #pragma unroll
         for (int j = 0; j < NTW; j++) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
-    AReg<WT> ar[IT];
+    AReg<AT> ar[IT];
 #pragma unroll
     for (int it = 0; it < IT; it++) {
         int item = tid + it * NT;
         asm volatile("" : "+v"(item));
-        if (item < ITEMS) a_store<WT, BM>(pre.ar[it], smem, item, unscale);
+        if (item < ITEMS) a_store<AT, BM>(pre.ar[it], smem, item, unscale);
     }
     // W fragments of the two blocks in flight: block b lives in wf[b & 1] and
     // is replaced by block b + 2 as soon as its MFMAs are issued
@@ -558,7 +578,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
             for (int it = 0; it < IT; it++) {
                 int item = tid + it * NT;
                 asm volatile("" : "+v"(item));
-                if (item < ITEMS) a_load<WT>(ar[it], args.A, K, m0, (kc + 1) * KC, item);
+                if (item < ITEMS) a_load<AT>(ar[it], args.A, K, m0, (kc + 1) * KC, item);
             }
         }
         const char *abuf = smem + (kc & 1) * A_BUF;
@@ -585,27 +605,49 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                     return TRANS ? __builtin_amdgcn_mfma_f32_16x16x32_f16(w, x, c, 0, 0, 0)
                                  : __builtin_amdgcn_mfma_f32_16x16x32_f16(x, w, c, 0, 0, 0);
                 };
+                // Q4_0N: the fragment's q - 8 as fp16 integers (one MFMA gives the
+                // block's isum exactly) and its d_w, per n-tile; the fold scales by
+                // d_a * d_w (exact in f32), as ggml_vec_dot_q4_0_q8_0
+                [[maybe_unused]] half8 wn[QN ? NTW : 1];
+                [[maybe_unused]] float4v dw[QN ? NTW : 1];
+                if constexpr (QN) {
+#pragma unroll
+                    for (int nt = 0; nt < NTW; nt++) {
+                        const u32x4v r = wf[kb & 1][nt].r;
+                        wn[nt] = nib_to_f16(r.x);
+                        if constexpr (TRANS)
+                            dw[nt] = float4v{h2f((uint16_t)r.y), h2f((uint16_t)(r.y >> 16)), h2f((uint16_t)r.z),
+                                             h2f((uint16_t)(r.z >> 16))};
+                        else
+                            dw[nt][0] = h2f((uint16_t)r.w);
+                    }
+                }
+                auto blk_of = [&](int rt_, int nt_) {
+                    if constexpr (QN) {
+                        return mfma(a[rt_], wn[nt_], zero4);
+                    } else {
+                        const float4v b = mfma(a[rt_], wf[kb & 1][nt_].hi, zero4);
+                        return mfma(a[rt_], wf[kb & 1][nt_].lo, b);
+                    }
+                };
 #pragma unroll
                 for (int rt = 0; rt < RT; rt++)
                     if (rt * NTW <= 1) lds_a(rt);
                 float4v blk[2];
-                blk[0] = mfma(a[0], wf[kb & 1][0].hi, zero4);
-                blk[0] = mfma(a[0], wf[kb & 1][0].lo, blk[0]);
+                blk[0] = blk_of(0, 0);
 #pragma unroll
                 for (int t = 0; t < T; t++) {
 #pragma unroll
                     for (int rt = 0; rt < RT; rt++)
                         if (rt * NTW == t + 2) lds_a(rt);
-                    if (t + 1 < T) {
-                        const int rt1 = (t + 1) / NTW, nt1 = (t + 1) % NTW;
-                        blk[(t + 1) & 1] = mfma(a[rt1], wf[kb & 1][nt1].hi, zero4);
-                        blk[(t + 1) & 1] = mfma(a[rt1], wf[kb & 1][nt1].lo, blk[(t + 1) & 1]);
-                    }
+                    if (t + 1 < T) blk[(t + 1) & 1] = blk_of((t + 1) / NTW, (t + 1) % NTW);
                     const int rt = t / NTW, nt = t % NTW;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         float v = acc[rt][nt][i];
-                        v = __builtin_fmaf(TRANS ? da[rt][0] : da[rt][i], blk[t & 1][i], v);
+                        float sc_i = TRANS ? da[rt][0] : da[rt][i];
+                        if constexpr (QN) sc_i *= TRANS ? dw[nt][i] : dw[nt][0];
+                        v = __builtin_fmaf(sc_i, blk[t & 1][i], v);
                         asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
                         acc[rt][nt][i] = v;
                     }
@@ -657,7 +699,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
             for (int it = 0; it < IT; it++) {
                 int item = tid + it * NT;
                 asm volatile("" : "+v"(item));
-                if (item < ITEMS) a_store<WT, BM>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
+                if (item < ITEMS) a_store<AT, BM>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
         __syncthreads();
@@ -672,7 +714,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int NTW = WN / 16;
     constexpr int NP = NTW / 2;  // column pairs per wave
     constexpr int RT = BM / 16;
-    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr bool QN = WT == W_Q4_0N, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
+    constexpr int AT = act_of(WT);
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
     constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
@@ -740,7 +783,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                             y[i] = h2f(gtab[f2h(fmaxf(b0[i] + acc[rt][2 * p][i], xlo))]);
                             y[4 + i] = h2f(gtab[f2h(fmaxf(b1[i] + acc[rt][2 * p + 1][i], xlo))]);
                         }
-                        store_act_quarter_t<WT>(args.out_act, args.N, mc + rt * 16 + c16, col >> 5, g, y);
+                        store_act_quarter_t<AT>(args.out_act, args.N, mc + rt * 16 + c16, col >> 5, g, y);
                     }
                 } else {
                     // F16 (plain pair-interleaved tile order, kernels.h WPtr): lane
@@ -923,11 +966,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
                         for (int j = 0; j < 4; j++)
                             y[4 * h + j] = h2f((uint16_t)gelu_lookup(tab, cap, f2h(gb[k][h][j] + v[j])));
                     }
-                    store_act_quarter<WT>(args.out_act, args.N, row0 + r, (n0 >> 5) + b, qq, y);
+                    store_act_quarter<AT>(args.out_act, args.N, row0 + r, (n0 >> 5) + b, qq, y);
                 }
             } else {
                 if (rt + 1 < RT) ln_xload<NBLK, NT>(xv[(rt + 1) & 1], tk, args.X, row0 + 16);
-                ln_row_phase_q<WT, NBLK, NT>(stage, LD, red, row0, tk, xv[rt & 1], args.X, args.ln_w, args.ln_b, args.eps,
+                ln_row_phase_q<AT, NBLK, NT>(stage, LD, red, row0, tk, xv[rt & 1], args.X, args.ln_w, args.ln_b, args.eps,
                                              args.out_act);
             }
         }
@@ -1244,7 +1287,7 @@ constexpr int QKVA_NW = 12;  // waves
 // int8 Q8_0 activations, context stored as Q8D for the fp6 O projection)
 template <int WT, int D, int NTW, bool PK, int CT = WT>
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
-    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr bool QN = WT == W_Q4_0N, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
     constexpr int NW = QKVA_NW, BM = 128, RT = BM / 16;
     constexpr int HU = 192 / (3 * D);  // heads per unit
     constexpr int NK = 128, KST = D + 8, VST = NK + 4;
@@ -1548,6 +1591,7 @@ hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a,
         case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, s);
         case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, s);
         case W_Q4_0D: return qkv_attn_w<W_Q4_0, W_Q4_0D>(g, a, n_blocks, s);
+        case W_Q4_0N: return qkv_attn_w<W_Q4_0N, W_Q4_0>(g, a, n_blocks, s);
         case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, s);
     }
     return hipErrorInvalidValue;
@@ -1813,7 +1857,12 @@ static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
 // 64 rows.  LayerNorm GEMMs own whole rows (BN = E).
 template <int WT>
 static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
-    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+    if constexpr (WT == W_Q4_0N) {  // the projections that read nibbles: QKV (unfused) and O + LN
+        if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
+        if (epi == EPI_LN && a.N == 384)
+            return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
+                                      : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
+    } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_GELU_ACT)  // 12 waves (3 per SIMD) where N allows; the GELU table fills the LDS
             return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)
@@ -1872,6 +1921,7 @@ hipError_t launch_gemm(int wtype, int epi, int /*unused*/, const GemmArgs &a, in
         case W_F16: return gemm_w<W_F16>(epi, a, Mpad, s);
         case W_Q4_0: return gemm_w<W_Q4_0>(epi, a, Mpad, s);
         case W_Q4_1: return gemm_w<W_Q4_1>(epi, a, Mpad, s);
+        case W_Q4_0N: return gemm_w<W_Q4_0N>(epi, a, Mpad, s);
     }
     return hipErrorInvalidValue;
 }

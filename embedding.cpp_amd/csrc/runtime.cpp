@@ -261,6 +261,9 @@ struct bert_ctx {
     // Q4_0 models whose O / FFN GEMMs run on the fp6 MFMA (gemm_f6.hip): their
     // activations are stored as Q8D (kernels.h W_Q4_0D); f6_select
     bool f6 = false;
+    // Q4_0 QKV (fused and unfused) and split-path O weights as nibbles,
+    // dequantised inside the fp16 MFMA GEMM (kernels.h W_Q4_0N); nib_select
+    bool q4nib = false;
     // run_pipeline knobs, read from the environment once at load
     // (BERT_AMD_SPLIT, BERT_AMD_PACK) and changed only by bert_amd_set_option:
     // two row groups on two streams (default on); fused-tile packing
@@ -302,7 +305,7 @@ struct Packed {
     float unscale = 1.f;
 };
 
-Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_t K) {
+Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_t K, bool nib = false) {
     const int64_t N = (int64_t)rows_in.size(), nkb = K / 32, ntl = N / 16;
     // column interleave (kernels.h WPtr): repacked tile 2p+t, lane column c
     // <- weight row 32p + 2c + t, i.e. repacked row 16*(2p+t) + c
@@ -311,7 +314,37 @@ Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_
         for (int t = 0; t < 2; t++)
             for (int c = 0; c < 16; c++) rows[(size_t)(32 * pr + 16 * t + c)] = rows_in[(size_t)(32 * pr + 2 * c + t)];
     Packed p;
-    if (type == GT_Q4_0 || type == GT_Q4_1) {
+    if (nib && type == GT_Q4_0) {
+        // kernels.h W_Q4_0N: per (n-tile, block) and lane (c, g) one 16-byte
+        // record {8 nibbles of row c, k = 8 g + j at bits 4 (j >> 1) + 16 (j & 1);
+        // fp16 d of rows 4g .. 4g + 3; fp16 d of row c}
+        p.q.resize((size_t)(ntl * nkb * 64 * 16));
+        uint32_t *q = (uint32_t *)p.q.data();
+        auto dh = [&](int64_t row, int64_t kb) {
+            uint16_t v;
+            std::memcpy(&v, rows[(size_t)row] + kb * 18, 2);
+            return (uint32_t)v;
+        };
+        for (int64_t nt = 0; nt < ntl; nt++)
+            for (int64_t kb = 0; kb < nkb; kb++)
+                for (int lane = 0; lane < 64; lane++) {
+                    const int c = lane & 15, g = lane >> 4;
+                    const uint8_t *blk = rows[(size_t)(nt * 16 + c)] + kb * 18;
+                    uint32_t x = 0;
+                    for (int j = 0; j < 8; j++) {
+                        const int e = 8 * g + j;
+                        const uint8_t byte = blk[2 + (e & 15)];
+                        const uint32_t qv = e < 16 ? (byte & 15u) : (byte >> 4);
+                        x |= qv << (4 * (j >> 1) + 16 * (j & 1));
+                    }
+                    uint32_t *r = &q[(size_t)(((nt * nkb + kb) * 64 + lane) * 4)];
+                    r[0] = x;
+                    r[1] = dh(nt * 16 + 4 * g, kb) | dh(nt * 16 + 4 * g + 1, kb) << 16;
+                    r[2] = dh(nt * 16 + 4 * g + 2, kb) | dh(nt * 16 + 4 * g + 3, kb) << 16;
+                    r[3] = dh(nt * 16 + c, kb);
+                }
+        p.unscale = 1.f;
+    } else if (type == GT_Q4_0 || type == GT_Q4_1) {
         // w = d*(q-8) | d*q + m, exact in double; scaled by 2^S so that
         // max|w| lands in [2^13, 2^14): the fp16 hi part stays far from
         // overflow and the lo part stays normal for all but negligible weights
@@ -664,6 +697,16 @@ void f6_select(bert_ctx *ctx) {
     if (ctx->f6) ctx->i8_o = ctx->i8_up = ctx->i8_down = false;
 }
 
+// Q4_0 QKV / O weights as nibbles with in-kernel dequant (kernels.h W_Q4_0N):
+// env BERT_AMD_Q4NIB=1 (read at load); not with the fp6 path, whose fused
+// kernel stores a Q8D context.
+void nib_select(bert_ctx *ctx) {
+    const char *e = std::getenv("BERT_AMD_Q4NIB");
+    ctx->q4nib = e && e[0] == '1' && ctx->wtype == W_Q4_0 && !ctx->f6 && ctx->hp.n_embd == 384;
+}
+// the weight type the QKV / split O launches name
+int qo_wtype(const bert_ctx *ctx) { return ctx->q4nib ? W_Q4_0N : ctx->wtype; }
+
 // One encoder layer over the row group [row0, row0 + rows) (sentences
 // d_off[0 .. nseq), absolute row offsets).  Xa / Ca / Ua / X point at the
 // group's first row; the QKV + attention kernels index rows absolutely through
@@ -709,9 +752,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(ctx->f6 ? W_Q4_0D : wt, qf, aa, ntiles, st));
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(ctx->f6 ? W_Q4_0D : qo_wtype(ctx), qf, aa, ntiles, st));
         } else {
-            LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
+            LAUNCH_OK("gemm_qkv", launch_gemm(qo_wtype(ctx), EPI_QKV, 0, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(act_type(ctx), D, aa, nseq, max_len, st));
         }
         if (ctx->f6) {  // O + LN, FFN up + GELU, FFN down + LN on the fp6 MFMA, Q8D in
@@ -771,7 +814,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
-            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)rows, st));
+            LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_LN, 0, o, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
@@ -1099,7 +1142,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
             for (size_t pr = 0; pr < rows.size() / 32; pr++)
                 for (int t = 0; t < 2; t++)
                     for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = quad[32 * pr + 16 * t + c];
-            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E))) return false;
+            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E, ctx->q4nib))) return false;
         }
         std::vector<const uint8_t *> up_rows = rows_of(l.i_w);
         if (gemm_gelu_blk8(ctx->wtype)) {
@@ -1111,13 +1154,14 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                 for (int t = 0; t < 2; t++)
                     for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
         }
-        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
+        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E, ctx->q4nib))) return false;
         // each projection in the one format its GEMM reads (fp6, int8 or split fp16)
         if (ctx->f6) {
             if (!upload_f6(tr, dl.o6, rows_of(l.o_w), E) || !upload_f6(tr, dl.up6, rows_of(l.i_w), E) ||
                 !upload_f6(tr, dl.down6, rows_of(l.o2_w), I))
                 return false;
-        } else if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E))) ||
+        } else if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E)
+                               : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E, ctx->q4nib))) ||
             !(ctx->i8_up ? upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) : upload_packed(tr, dl.up, repack(wt, up_rows, E))) ||
             !(ctx->i8_down ? upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I)
                            : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))))
@@ -1293,6 +1337,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     }
     i8_select(ctx.get());
     f6_select(ctx.get());
+    nib_select(ctx.get());
     if (const char *e = std::getenv("BERT_AMD_SPLIT")) ctx->split = e[0] != '0';
     if (const char *e = std::getenv("BERT_AMD_PACK")) ctx->pack = e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
     if (const char *e = std::getenv("BERT_AMD_FUSE_MIN")) ctx->fuse_min = std::max(0, std::atoi(e));

@@ -135,6 +135,32 @@ def test_int8_gemm_path_golden(case, mode, model_dir, monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01"])
+def test_q4_nibble_qkv_o_golden(case, model_dir, monkeypatch):
+    """QKV (fused and unfused) and O-projection weights as ggml nibbles,
+    dequantised inside the fp16 MFMA GEMM (env BERT_AMD_Q4NIB=1, kernels.h
+    W_Q4_0N: one MFMA gives the block's exact isum, the fold applies
+    d_w * d_a per block like ggml_vec_dot_q4_0_q8_0): golden fixtures within
+    the bound, deterministic, and the fused kernel bitwise the unfused pair."""
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    monkeypatch.setenv("BERT_AMD_Q4NIB", "1")
+    m = bertlib.BertModel(p)
+    try:
+        got = m.eval_batch(toks)
+        assert np.array_equal(got, m.eval_batch(toks))
+        short = [t for t in toks if len(t) <= 128] * 8  # >= fuse_min: the fused kernel
+        m.set_option("fuse_min", 0)
+        fused = m.eval_batch(short)
+        m.set_option("fuse_min", 10 ** 6)
+        assert np.array_equal(m.eval_batch(short), fused)
+    finally:
+        m.close()
+    c = cos(got, want)
+    print(f"BERT_AMD_Q4NIB=1 {case}: 1-cos max {1 - c.min():.2e}")
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
+
+
+@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01"])
 def test_fp6_gemm_path_bitwise_int8(case, model_dir, monkeypatch):
     """O / FFN-up / FFN-down on the fp6-MFMA GEMMs (env BERT_AMD_F6=1:
     gemm_f6.hip, Q8D activations, isum as two exact fp6 digit-plane MFMAs,
