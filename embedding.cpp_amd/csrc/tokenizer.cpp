@@ -262,7 +262,52 @@ bool WordPieceTokenizer::load(const std::string &json, std::string &err) {
         }
     std::sort(added_.begin(), added_.end(), [](auto &a, auto &b) { return a.first.size() > b.first.size(); });
     if (!vocab_.count(unk_)) { err = "tokenizer.json: unk token not in vocab"; return false; }
+    unk_id_ = vocab_.at(unk_);
+    for (auto &a : added_) added_first_[(unsigned char)a.first[0]] = true;
+    // the ASCII fast path's tables, from the same predicates normalize() and
+    // pre_tokenize() apply (NFD and accent stripping are the identity on ASCII)
+    for (uint32_t c = 0; c < 128; c++) {
+        uint32_t n = c;
+        bool drop = false;
+        if (clean_text_) {
+            if (c == 0 || is_control(c)) drop = true;
+            else if (is_whitespace(c)) n = ' ';
+        }
+        if (!drop && lowercase_)
+            if (const uint32_t *m = find_map(kLower, n)) n = m[1];
+        ascii_norm_[c] = (uint8_t)n;
+        ascii_class_[c] = drop ? 0 : is_whitespace(n) ? 1 : is_punct(n) ? 2 : 3;
+    }
     return true;
+}
+
+// WordPiece on one pre-token w of nchars characters (byte offset of char k:
+// off[k]): greedy longest match from the left, "##" continuations, [UNK] for
+// the whole word if any piece is missing.  `buf` is scratch.
+void WordPieceTokenizer::wordpiece(const std::string &w, size_t nchars, const size_t *off, std::vector<int32_t> &ids,
+                                   std::string &buf) const {
+    if ((int)nchars > max_chars_) { ids.push_back(unk_id_); return; }
+    const size_t base = ids.size();
+    size_t start = 0;
+    while (start < nchars) {
+        size_t end = nchars;
+        int32_t found = -1;
+        while (start < end) {
+            buf.clear();
+            if (start > 0) buf += prefix_;
+            buf.append(w, off[start], off[end] - off[start]);
+            auto it = vocab_.find(buf);
+            if (it != vocab_.end()) { found = it->second; break; }
+            end--;
+        }
+        if (found < 0) {
+            ids.resize(base);
+            ids.push_back(unk_id_);
+            return;
+        }
+        ids.push_back(found);
+        start = end;
+    }
 }
 
 std::string WordPieceTokenizer::normalize(const std::string &text) const {
@@ -323,13 +368,14 @@ std::vector<std::string> WordPieceTokenizer::pre_tokenize(const std::string &nor
 
 std::vector<int32_t> WordPieceTokenizer::encode(const std::string &text) const {
     std::vector<int32_t> ids;
-    const int32_t unk = vocab_.at(unk_);
+    const int32_t unk = unk_id_;
     // split out added (special) tokens first: they are never normalised
     std::vector<std::pair<std::string, int32_t>> pieces;  // id >= 0: special token
     {
         size_t i = 0, start = 0;
         while (i < text.size()) {
             bool hit = false;
+            if (added_first_[(unsigned char)text[i]])
             for (auto &a : added_) {
                 if (text.compare(i, a.first.size(), a.first) == 0) {
                     if (i > start) pieces.emplace_back(text.substr(start, i - start), -1);
@@ -344,8 +390,37 @@ std::vector<int32_t> WordPieceTokenizer::encode(const std::string &text) const {
         }
         if (start < text.size()) pieces.emplace_back(text.substr(start), -1);
     }
+    std::string buf, word;
+    std::vector<size_t> aoff;
     for (auto &pc : pieces) {
         if (pc.second >= 0) { ids.push_back(pc.second); continue; }
+        const std::string &t = pc.first;
+        if (std::all_of(t.begin(), t.end(), [](char ch) { return (unsigned char)ch < 0x80; })) {
+            // ASCII: normalise, split and look up in one pass, one byte per char
+            auto flush = [&]() {
+                if (word.empty()) return;
+                if (aoff.size() < word.size() + 1) {
+                    aoff.resize(word.size() + 1);
+                    for (size_t k = 0; k < aoff.size(); k++) aoff[k] = k;
+                }
+                wordpiece(word, word.size(), aoff.data(), ids, buf);
+                word.clear();
+            };
+            for (char ch : t) {
+                const uint8_t c = (uint8_t)ch, cls = ascii_class_[c];
+                if (cls == 0) continue;
+                if (cls == 1) { flush(); continue; }
+                if (cls == 2) {
+                    flush();
+                    word.assign(1, (char)ascii_norm_[c]);
+                    flush();
+                    continue;
+                }
+                word += (char)ascii_norm_[c];
+            }
+            flush();
+            continue;
+        }
         for (const std::string &w : pre_tokenize(normalize(pc.first))) {
             const std::vector<uint32_t> chars = utf8_decode(w);
             if ((int)chars.size() > max_chars_) { ids.push_back(unk); continue; }

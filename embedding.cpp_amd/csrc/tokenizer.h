@@ -39,6 +39,14 @@ private:
     int32_t pad_id_ = 0;
     // added (special) tokens are matched verbatim before normalisation
     std::vector<std::pair<std::string, int32_t>> added_;
+    bool added_first_[256] = {};  // first bytes of the added tokens
+    int32_t unk_id_ = 0;
+    // ASCII fast path (byte-for-byte the general path's decisions, tabulated
+    // at load): 0 drop, 1 whitespace, 2 punctuation, 3 word character; and the
+    // byte after normalisation
+    uint8_t ascii_class_[128] = {}, ascii_norm_[128] = {};
+    void wordpiece(const std::string &w, size_t nchars, const size_t *off, std::vector<int32_t> &ids,
+                   std::string &buf) const;
 };
 
 }  // namespace bertamd
