@@ -451,7 +451,7 @@ def main():
     # framed), host tokenisation and host buffers included, against the same
     # sentences device-resident in one batch
     consumer = None
-    if args.consumer_texts > 0:
+    if args.consumer_texts > 0 and rank == 0:
         log("consumer path timing (bert_encode_batch)")
         consumer = consumer_line(model, hp, args.consumer_texts, rank, dev, stream, torch)
 
