@@ -377,9 +377,9 @@ struct AReg {
     float d;
 };
 
-template <int WT>
+template <int WT, int KBT = KB>
 __device__ __forceinline__ void a_load(AReg<WT> &ar, const ActPtr &A, int K, int64_t m0, int k0, int item) {
-    const int r = item >> 2, s = item & 3;
+    const int r = item / (2 * KBT), s = item % (2 * KBT);  // 2 KBT 16-element pieces per chunk row
     const int64_t row = m0 + r;
     const int k = k0 + s * 16;
     if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
@@ -413,9 +413,9 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t x, half2v &lo, half2v &hi) 
     hi = __builtin_bit_cast(half2v, h) - off;
 }
 
-template <int WT, int BM, int LDA = LDA_H>
+template <int WT, int BM, int LDA = LDA_H, int KBT = KB>
 __device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item, float unscale) {
-    const int r = item >> 2, s = item & 3;
+    const int r = item / (2 * KBT), s = item % (2 * KBT);
     constexpr int A_BYTES = (WT == W_F32) ? BM * LDA_F * 4 : BM * LDA * 2;
     if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         const u32x4v w = ar.r[0];
@@ -500,17 +500,17 @@ __device__ __forceinline__ half8 nib_to_f16(uint32_t x) {
 // The loop's first loads (A chunk 0 into registers, W blocks 0 and 1) come
 // from a MainloopPre the caller filled with mainloop_preload, early enough
 // for their latency to hide behind other work where it can.
-template <int WT, int NW, int BM, int NTW>
+template <int WT, int NW, int BM, int NTW, int KBT = KB>
 struct MainloopPre {
-    static constexpr int IT = (BM * (KC / 16) + NW * 64 - 1) / (NW * 64);
+    static constexpr int IT = (BM * (2 * KBT) + NW * 64 - 1) / (NW * 64);
     AReg<act_of(WT)> ar[IT];
     WFrag<WT> wf[WT == W_F32 ? 1 : 2][NTW];
 };
 
-template <int WT, int NW, int BM, int NTW>
-__device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW> &pre, const GemmArgs &args, int64_t m0,
-                                                 int64_t ntile0) {
-    constexpr int NT = NW * 64, ITEMS = BM * (KC / 16), IT = MainloopPre<WT, NW, BM, NTW>::IT;
+template <int WT, int NW, int BM, int NTW, int KBT = KB>
+__device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW, KBT> &pre, const GemmArgs &args,
+                                                 int64_t m0, int64_t ntile0) {
+    constexpr int NT = NW * 64, ITEMS = BM * (2 * KBT), IT = MainloopPre<WT, NW, BM, NTW, KBT>::IT;
     const int tid = threadIdx.x, nkb = args.K >> 5;
 #pragma unroll
     for (int it = 0; it < IT; it++) {
@@ -520,7 +520,7 @@ __device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW> &p
         // scratch 64 -> 20 bytes per lane)
         int item = tid + it * NT;
         asm volatile("" : "+v"(item));
-        if (item < ITEMS) a_load<act_of(WT)>(pre.ar[it], args.A, args.K, m0, 0, item);
+        if (item < ITEMS) a_load<act_of(WT), KBT>(pre.ar[it], args.A, args.K, m0, 0, item);
     }
     if constexpr (WT != W_F32) {
 #pragma unroll
@@ -530,10 +530,14 @@ __device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW> &p
     }
 }
 
-template <int WT, int NW, int BM, int NTW, bool TRANS = false>
+template <int WT, int NW, int BM, int NTW, bool TRANS = false, int KBT = KB>
 __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, int64_t ntile0, char *smem,
-                                              float4v (&acc)[BM / 16][NTW], const MainloopPre<WT, NW, BM, NTW> &pre) {
+                                              float4v (&acc)[BM / 16][NTW],
+                                              const MainloopPre<WT, NW, BM, NTW, KBT> &pre) {
     static_assert(!TRANS || WT != W_F32, "transposed main loop: fp16 MFMA formats only");
+    static_assert(KBT == KB || WT != W_F32, "f32 main loop: the global chunk only");
+    // KBT 32-wide blocks per chunk (one barrier per chunk)
+    constexpr int KB = KBT, KC = 32 * KBT, LDA_H = KC + (KBT == 2 ? 16 : 8);
     constexpr int NT = NW * 64;
     constexpr int RT = BM / 16;
     constexpr bool QN = WT == W_Q4_0N, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
@@ -557,7 +561,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     for (int it = 0; it < IT; it++) {
         int item = tid + it * NT;
         asm volatile("" : "+v"(item));
-        if (item < ITEMS) a_store<AT, BM>(pre.ar[it], smem, item, unscale);
+        if (item < ITEMS) a_store<AT, BM, LDA_H, KBT>(pre.ar[it], smem, item, unscale);
     }
     // W fragments of the two blocks in flight: block b lives in wf[b & 1] and
     // is replaced by block b + 2 as soon as its MFMAs are issued
@@ -578,7 +582,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
             for (int it = 0; it < IT; it++) {
                 int item = tid + it * NT;
                 asm volatile("" : "+v"(item));
-                if (item < ITEMS) a_load<AT>(ar[it], args.A, K, m0, (kc + 1) * KC, item);
+                if (item < ITEMS) a_load<AT, KBT>(ar[it], args.A, K, m0, (kc + 1) * KC, item);
             }
         }
         const char *abuf = smem + (kc & 1) * A_BUF;
@@ -699,7 +703,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
             for (int it = 0; it < IT; it++) {
                 int item = tid + it * NT;
                 asm volatile("" : "+v"(item));
-                if (item < ITEMS) a_store<AT, BM>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
+                if (item < ITEMS) a_store<AT, BM, LDA_H, KBT>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
         __syncthreads();
@@ -1280,6 +1284,9 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 // half of the context) at D = 64 (the two halves share the scores, computed
 // by both waves).
 constexpr int QKVA_NW = 12;  // waves
+#ifndef QKVA_KB
+#define QKVA_KB 2  // 32-wide blocks per main-loop chunk in the fused kernel
+#endif
 
 // D: head dim; NTW: 192-feature units per main loop (qkv_attention_ntw); PK:
 // sentence tiles (a.tiles)
@@ -1291,7 +1298,8 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     constexpr int NW = QKVA_NW, BM = 128, RT = BM / 16;
     constexpr int HU = 192 / (3 * D);  // heads per unit
     constexpr int NK = 128, KST = D + 8, VST = NK + 4;
-    constexpr int A_BUF = (WT == W_F32 ? BM * LDA_F * 4 : BM * LDA_H * 2) + (QP ? KB * BM * 4 : 0);
+    constexpr int QKB = QKVA_KB, QLDA = 32 * QKB + (QKB == 2 ? 16 : 8);
+    constexpr int A_BUF = BM * QLDA * 2 + (QP ? QKB * BM * 4 : 0);
     constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
     constexpr int SMEM = (2 * A_BUF > HU * SLOT) ? 2 * A_BUF : HU * SLOT;
     static_assert(NW * 16 == HU * 3 * D, "one 16-feature n-tile per wave covers a unit");
@@ -1361,12 +1369,12 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
         // plays the one-unit role of the split below.
         const int64_t nt0 = (int64_t)qd * NTW * NW + NTW * wv;
         float4v acc[RT][NTW];
-        MainloopPre<WT, NW, BM, NTW> pre;
+        MainloopPre<WT, NW, BM, NTW, QKB> pre;
         mainloop_preload(pre, g, beg, nt0);
         if (part_w == 2)  // ends with a barrier
-            gemm_mainloop<WT, NW, BM, NTW, false>(g, beg, nt0, smem, acc, pre);
+            gemm_mainloop<WT, NW, BM, NTW, false, QKB>(g, beg, nt0, smem, acc, pre);
         else
-            gemm_mainloop<WT, NW, BM, NTW, true>(g, beg, nt0, smem, acc, pre);
+            gemm_mainloop<WT, NW, BM, NTW, true, QKB>(g, beg, nt0, smem, acc, pre);
 #pragma unroll
         for (int half = 0; half < NTW; half++) {
             const int pr = NTW * qd + half;
