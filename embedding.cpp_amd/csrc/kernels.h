@@ -28,10 +28,11 @@ namespace bertamd {
 // W_Q4_0D: Q4_0 weights whose GEMMs run on the block-scaled fp6 MFMA
 // (gemm_f6.hip); the same ggml Q8_0 activations (d, q), stored as Q8D: per
 // 32-block 48 bytes of fp6 digit codes (kernels_common.h q8d_*) + fp16 d.
-enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3, W_Q4_0D = 4, W_Q4_0N = 5 };
-// W_Q4_0N: Q4_0 weights kept as ggml's nibbles and dequantised inside the fp16
-// MFMA GEMM (WPtr below); its activations are Q4_0's (ggml Q8_0).
-constexpr int act_of(int wt) { return wt == W_Q4_0N ? W_Q4_0 : wt; }
+enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3, W_Q4_0D = 4, W_Q4_0N = 5, W_Q4_1N = 6 };
+// W_Q4_0N / W_Q4_1N: Q4 weights kept as ggml's nibbles and dequantised inside
+// the fp16 MFMA GEMM (WPtr below); their activations are Q4_0's / Q4_1's
+// (ggml Q8_0 / Q8_1).
+constexpr int act_of(int wt) { return wt == W_Q4_0N ? W_Q4_0 : wt == W_Q4_1N ? W_Q4_1 : wt; }
 constexpr int Q8D_BLK = 48;  // code bytes per Q8D block
 
 struct ActPtr {
@@ -56,6 +57,10 @@ struct ActPtr {
 //         The MFMA takes q - 8 as exact fp16 integers against the Q8 codes
 //         (isum exact in f32) and the fold applies d_w * d_a per block, as
 //         ggml_vec_dot_q4_0_q8_0; 0.56 B per weight.
+//   Q4_1N: q = uint32 [N/16][K/32][64][2] (plain main loop only): the 8
+//         nibbles q (same bit order as Q4_0N) and the fp16 d | m << 16 of
+//         column c; the fold adds ggml's m_w * s_a term per block
+//         (vec_dot_q4_1_q8_1: d_w d_a isum + m_w s_a, s_a = d_a sum(q_a)).
 //   F16 : q = fp16 [N/16][K/32][64][8]
 //   F32 : q = f32  [N/16][K/32][64][8]
 struct WPtr {

@@ -413,7 +413,9 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t x, half2v &lo, half2v &hi) 
     hi = __builtin_bit_cast(half2v, h) - off;
 }
 
-template <int WT, int BM, int LDA = LDA_H, int KBT = KB>
+// SA (Q4_1N GEMMs): also s_a = d_a * sum(q_a) per (block, row), after the d_a
+// array (ggml's block_q8_1 s term); the block's two pieces are lanes l, l ^ 1.
+template <int WT, int BM, int LDA = LDA_H, int KBT = KB, bool SA = false>
 __device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item, float unscale) {
     const int r = item / (2 * KBT), s = item % (2 * KBT);
     constexpr int A_BYTES = (WT == W_F32) ? BM * LDA_F * 4 : BM * LDA * 2;
@@ -432,6 +434,15 @@ __device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item,
         half8 *dst = (half8 *)((_Float16 *)buf + r * LDA + s * 16);
         dst[0] = h0;
         dst[1] = h1;
+        if constexpr (SA) {
+            int q = 0;
+            q = __builtin_amdgcn_sdot4((int)w.x, 0x01010101, q, false);
+            q = __builtin_amdgcn_sdot4((int)w.y, 0x01010101, q, false);
+            q = __builtin_amdgcn_sdot4((int)w.z, 0x01010101, q, false);
+            q = __builtin_amdgcn_sdot4((int)w.w, 0x01010101, q, false);
+            q += __shfl_xor(q, 1);
+            if ((s & 1) == 0) ((float *)(buf + A_BYTES))[KBT * BM + (s >> 1) * BM + r] = ar.d * (float)q;
+        }
         if ((s & 1) == 0) {
             float *sc = (float *)(buf + A_BYTES);  // [block of the chunk][BM]: d_a * 2^-S (exact)
             sc[(s >> 1) * BM + r] = ar.d * unscale;
@@ -454,6 +465,8 @@ template <> struct WFrag<W_Q4_0> { half8 hi, lo; };
 // Q4_0N: one 16-byte record per lane: 8 nibbles, the fp16 d_w of columns
 // 4g .. 4g + 3 (transposed main loop) and of column c16 (plain)
 template <> struct WFrag<W_Q4_0N> { u32x4v r; };
+// Q4_1N: 8 nibbles and the column's fp16 d | m << 16
+template <> struct WFrag<W_Q4_1N> { u32x2v r; };
 template <> struct WFrag<W_Q4_1> { half8 hi, lo; };
 template <> struct WFrag<W_F16> { half8 h; };
 template <> struct WFrag<W_F32> { float4v f[2]; };
@@ -462,7 +475,9 @@ template <int WT>
 __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
     const int lane = threadIdx.x & 63;
     WFrag<WT> f;
-    if constexpr (WT == W_Q4_0N) {
+    if constexpr (WT == W_Q4_1N) {
+        f.r = ((const u32x2v *)W.q)[tile * 64 + lane];
+    } else if constexpr (WT == W_Q4_0N) {
         f.r = ((const u32x4v *)W.q)[tile * 64 + lane];
     } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         f.hi = ((const half8 *)W.q)[(tile * 2) * 64 + lane];
@@ -478,8 +493,10 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
 
 // Q4_0N: 8 nibbles (k = 2 s + e at bits 4 s + 16 e) -> q - 8 as exact fp16
 // integers: (0x6400 | q) is 1024 + q, one and-or and one packed subtract per pair
+// (Q4_1N: q itself, OFF = 1024)
+template <int OFF = 1032>
 __device__ __forceinline__ half8 nib_to_f16(uint32_t x) {
-    const half2v off = {(_Float16)1032.f, (_Float16)1032.f};
+    const half2v off = {(_Float16)(float)OFF, (_Float16)(float)OFF};
     half8 w;
 #pragma unroll
     for (int s = 0; s < 4; s++) {
@@ -540,11 +557,12 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     constexpr int KB = KBT, KC = 32 * KBT, LDA_H = KC + (KBT == 2 ? 16 : 8);
     constexpr int NT = NW * 64;
     constexpr int RT = BM / 16;
-    constexpr bool QN = WT == W_Q4_0N, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
+    constexpr bool QN1 = WT == W_Q4_1N, QN = WT == W_Q4_0N || QN1, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
+    static_assert(!QN1 || !TRANS, "Q4_1N: plain main loop only");
     constexpr int AT = act_of(WT);
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
-    constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
+    constexpr int A_BUF = A_BYTES + (QP ? (QN1 ? 2 : 1) * KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
     const int tid = threadIdx.x, lane = tid & 63;
@@ -561,7 +579,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     for (int it = 0; it < IT; it++) {
         int item = tid + it * NT;
         asm volatile("" : "+v"(item));
-        if (item < ITEMS) a_store<AT, BM, LDA_H, KBT>(pre.ar[it], smem, item, unscale);
+        if (item < ITEMS) a_store<AT, BM, LDA_H, KBT, QN1>(pre.ar[it], smem, item, unscale);
     }
     // W fragments of the two blocks in flight: block b lives in wf[b & 1] and
     // is replaced by block b + 2 as soon as its MFMAs are issued
@@ -598,8 +616,10 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 const float *sc = (const float *)(abuf + A_BYTES) + kb * BM;
                 half8 a[RT];
                 float4v da[RT];  // TRANS: da[rt][0] = d_a of row 16 rt + c16
+                [[maybe_unused]] float4v sa[QN1 ? RT : 1];  // Q4_1N: s_a of the lane's rows
                 auto lds_a = [&](int rt) {
                     a[rt] = *(const half8 *)((const _Float16 *)abuf + (rt * 16 + c16) * LDA_H + kb * 32 + 8 * g);
+                    if constexpr (QN1) sa[rt] = *(const float4v *)(sc + KB * BM + rt * 16 + g * 4);
                     if constexpr (TRANS)
                         da[rt][0] = sc[rt * 16 + c16];
                     else
@@ -614,7 +634,15 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 // d_a * d_w (exact in f32), as ggml_vec_dot_q4_0_q8_0
                 [[maybe_unused]] half8 wn[QN ? NTW : 1];
                 [[maybe_unused]] float4v dw[QN ? NTW : 1];
-                if constexpr (QN) {
+                if constexpr (QN1) {  // Q4_1N: q as fp16 integers, d_w and m_w of the lane's column
+#pragma unroll
+                    for (int nt = 0; nt < NTW; nt++) {
+                        const u32x2v r = wf[kb & 1][nt].r;
+                        wn[nt] = nib_to_f16<1024>(r.x);
+                        dw[nt][0] = h2f((uint16_t)r.y);
+                        dw[nt][1] = h2f((uint16_t)(r.y >> 16));
+                    }
+                } else if constexpr (QN) {
 #pragma unroll
                     for (int nt = 0; nt < NTW; nt++) {
                         const u32x4v r = wf[kb & 1][nt].r;
@@ -652,6 +680,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                         float sc_i = TRANS ? da[rt][0] : da[rt][i];
                         if constexpr (QN) sc_i *= TRANS ? dw[nt][i] : dw[nt][0];
                         v = __builtin_fmaf(sc_i, blk[t & 1][i], v);
+                        if constexpr (QN1) v = __builtin_fmaf(dw[nt][1], sa[rt][i], v);  // + m_w s_a
                         asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
                         acc[rt][nt][i] = v;
                     }
@@ -703,7 +732,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
             for (int it = 0; it < IT; it++) {
                 int item = tid + it * NT;
                 asm volatile("" : "+v"(item));
-                if (item < ITEMS) a_store<AT, BM, LDA_H, KBT>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
+                if (item < ITEMS) a_store<AT, BM, LDA_H, KBT, QN1>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
         __syncthreads();
@@ -718,11 +747,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int NTW = WN / 16;
     constexpr int NP = NTW / 2;  // column pairs per wave
     constexpr int RT = BM / 16;
-    constexpr bool QN = WT == W_Q4_0N, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
+    constexpr bool QN1 = WT == W_Q4_1N, QN = WT == W_Q4_0N || QN1, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
     constexpr int AT = act_of(WT);
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
-    constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
+    constexpr int A_BUF = A_BYTES + (QP ? (QN1 ? 2 : 1) * KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
     // Q4 / F16 GELU: transposed accumulators (Q4: in block-8 column order,
@@ -1865,11 +1894,12 @@ static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
 // 64 rows.  LayerNorm GEMMs own whole rows (BN = E).
 template <int WT>
 static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
-    if constexpr (WT == W_Q4_0N) {  // the projections that read nibbles: QKV (unfused) and O + LN
+    if constexpr (WT == W_Q4_0N || WT == W_Q4_1N) {  // nibble weights: QKV (unfused), O / down (+ LN or residual)
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_LN && a.N == 384)
             return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
                                       : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
+        if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
     } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_GELU_ACT)  // 12 waves (3 per SIMD) where N allows; the GELU table fills the LDS
@@ -1930,6 +1960,7 @@ hipError_t launch_gemm(int wtype, int epi, int /*unused*/, const GemmArgs &a, in
         case W_Q4_0: return gemm_w<W_Q4_0>(epi, a, Mpad, s);
         case W_Q4_1: return gemm_w<W_Q4_1>(epi, a, Mpad, s);
         case W_Q4_0N: return gemm_w<W_Q4_0N>(epi, a, Mpad, s);
+        case W_Q4_1N: return gemm_w<W_Q4_1N>(epi, a, Mpad, s);
     }
     return hipErrorInvalidValue;
 }

@@ -314,7 +314,30 @@ Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_
         for (int t = 0; t < 2; t++)
             for (int c = 0; c < 16; c++) rows[(size_t)(32 * pr + 16 * t + c)] = rows_in[(size_t)(32 * pr + 2 * c + t)];
     Packed p;
-    if (nib && type == GT_Q4_0) {
+    if (nib && type == GT_Q4_1) {
+        // kernels.h W_Q4_1N: per (n-tile, block) and lane (c, g) one 8-byte
+        // record {8 nibbles q of row c, k = 8 g + j at bits 4 (j >> 1) + 16 (j & 1);
+        // fp16 d | m << 16 of row c}
+        p.q.resize((size_t)(ntl * nkb * 64 * 8));
+        uint32_t *q = (uint32_t *)p.q.data();
+        for (int64_t nt = 0; nt < ntl; nt++)
+            for (int64_t kb = 0; kb < nkb; kb++)
+                for (int lane = 0; lane < 64; lane++) {
+                    const int c = lane & 15, g = lane >> 4;
+                    const uint8_t *blk = rows[(size_t)(nt * 16 + c)] + kb * 20;
+                    uint32_t x = 0;
+                    for (int j = 0; j < 8; j++) {
+                        const int e = 8 * g + j;
+                        const uint8_t byte = blk[4 + (e & 15)];
+                        const uint32_t qv = e < 16 ? (byte & 15u) : (byte >> 4);
+                        x |= qv << (4 * (j >> 1) + 16 * (j & 1));
+                    }
+                    uint32_t *r = &q[(size_t)(((nt * nkb + kb) * 64 + lane) * 2)];
+                    r[0] = x;
+                    std::memcpy(&r[1], blk, 4);  // d, m (fp16, little-endian: d in the low half)
+                }
+        p.unscale = 1.f;
+    } else if (nib && type == GT_Q4_0) {
         // kernels.h W_Q4_0N: per (n-tile, block) and lane (c, g) one 16-byte
         // record {8 nibbles of row c, k = 8 g + j at bits 4 (j >> 1) + 16 (j & 1);
         // fp16 d of rows 4g .. 4g + 3; fp16 d of row c}
@@ -697,15 +720,24 @@ void f6_select(bert_ctx *ctx) {
     if (ctx->f6) ctx->i8_o = ctx->i8_up = ctx->i8_down = false;
 }
 
-// Q4_0 QKV / O weights as nibbles with in-kernel dequant (kernels.h W_Q4_0N):
-// env BERT_AMD_Q4NIB=1 (read at load); not with the fp6 path, whose fused
-// kernel stores a Q8D context.
+// Q4 weights as nibbles with in-kernel dequant (kernels.h W_Q4_0N / W_Q4_1N):
+// env BERT_AMD_Q4NIB=1 (read at load).  Q4_0 (n_embd 384): the QKV (fused and
+// unfused) and O weights; not with the fp6 path, whose fused kernel stores a
+// Q8D context.  Q4_1: the unfused QKV and the split-path O and FFN-down
+// weights (the fused QKV + attention kernel keeps the split planes).
 void nib_select(bert_ctx *ctx) {
     const char *e = std::getenv("BERT_AMD_Q4NIB");
-    ctx->q4nib = e && e[0] == '1' && ctx->wtype == W_Q4_0 && !ctx->f6 && ctx->hp.n_embd == 384;
+    const bool on = e && e[0] == '1';
+    ctx->q4nib = on && ((ctx->wtype == W_Q4_0 && !ctx->f6 && ctx->hp.n_embd == 384) || ctx->wtype == W_Q4_1);
 }
-// the weight type the QKV / split O launches name
-int qo_wtype(const bert_ctx *ctx) { return ctx->q4nib ? W_Q4_0N : ctx->wtype; }
+// the weight type the unfused QKV / split O / split down launches name
+int qo_wtype(const bert_ctx *ctx) {
+    return !ctx->q4nib ? ctx->wtype : ctx->wtype == W_Q4_0 ? W_Q4_0N : W_Q4_1N;
+}
+// the split-path FFN-down weight type
+int down_wtype(const bert_ctx *ctx) { return ctx->q4nib && ctx->wtype == W_Q4_1 ? W_Q4_1N : ctx->wtype; }
+// the fused QKV + attention kernel's weight type
+int qkv_fused_wtype(const bert_ctx *ctx) { return ctx->f6 ? W_Q4_0D : ctx->wtype == W_Q4_0 ? qo_wtype(ctx) : ctx->wtype; }
 
 // One encoder layer over the row group [row0, row0 + rows) (sentences
 // d_off[0 .. nseq), absolute row offsets).  Xa / Ca / Ua / X point at the
@@ -752,7 +784,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(ctx->f6 ? W_Q4_0D : qo_wtype(ctx), qf, aa, ntiles, st));
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(qkv_fused_wtype(ctx), qf, aa, ntiles, st));
         } else {
             LAUNCH_OK("gemm_qkv", launch_gemm(qo_wtype(ctx), EPI_QKV, 0, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(act_type(ctx), D, aa, nseq, max_len, st));
@@ -816,7 +848,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         } else if (ln_fused) {
             LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_LN, 0, o, (int)rows, st));
         } else {
-            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)rows, st));
+            LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_RESID, 0, o, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
         }
 
@@ -857,9 +889,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
-            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)rows, st));
+            LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_LN, 0, dn, (int)rows, st));
         } else {
-            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)rows, st));
+            LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_RESID, 0, dn, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
         }
     }
@@ -1142,7 +1174,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
             for (size_t pr = 0; pr < rows.size() / 32; pr++)
                 for (int t = 0; t < 2; t++)
                     for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = quad[32 * pr + 16 * t + c];
-            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E, ctx->q4nib))) return false;
+            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E, ctx->q4nib && wt == GT_Q4_0))) return false;
         }
         std::vector<const uint8_t *> up_rows = rows_of(l.i_w);
         if (gemm_gelu_blk8(ctx->wtype)) {
@@ -1164,7 +1196,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                                : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E, ctx->q4nib))) ||
             !(ctx->i8_up ? upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) : upload_packed(tr, dl.up, repack(wt, up_rows, E))) ||
             !(ctx->i8_down ? upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I)
-                           : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))))
+                           : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I, down_wtype(ctx) == W_Q4_1N))))
             return false;
         if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
             !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||

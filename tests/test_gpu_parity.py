@@ -160,6 +160,29 @@ def test_q4_nibble_qkv_o_golden(case, model_dir, monkeypatch):
     assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
 
 
+@pytest.mark.parametrize("case", ["c5_bge_q4_1_l2", "c5_bge_q4_1_l2_short", "minilm_q4_1"])
+def test_q4_1_nibble_golden(case, model_dir, monkeypatch):
+    """Q4_1 unfused-QKV, split O and FFN-down weights as ggml nibbles (env
+    BERT_AMD_Q4NIB=1, kernels.h W_Q4_1N: one MFMA gives the block's exact
+    isum of q_w * q_a, the fold adds d_w d_a isum + m_w s_a per block like
+    ggml_vec_dot_q4_1_q8_1): golden fixtures within the bound, deterministic,
+    small batches (unfused path) bitwise the same rows in a full batch."""
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    monkeypatch.setenv("BERT_AMD_Q4NIB", "1")
+    m = bertlib.BertModel(p)
+    try:
+        m.set_option("fuse_min", 10 ** 6)  # every batch on the unfused QKV GEMM (nibbles)
+        got = m.eval_batch(toks)
+        assert np.array_equal(got, m.eval_batch(toks))
+        assert np.array_equal(m.eval_batch(toks[:3]), got[:3])
+    finally:
+        m.close()
+    c = cos(got, want)
+    print(f"BERT_AMD_Q4NIB=1 {case}: 1-cos max {1 - c.min():.2e}")
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
+
+
 @pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01"])
 def test_fp6_gemm_path_bitwise_int8(case, model_dir, monkeypatch):
     """O / FFN-up / FFN-down on the fp6-MFMA GEMMs (env BERT_AMD_F6=1:
