@@ -517,6 +517,11 @@ __device__ __forceinline__ half8 nib_to_f16(uint32_t x) {
 // The loop's first loads (A chunk 0 into registers, W blocks 0 and 1) come
 // from a MainloopPre the caller filled with mainloop_preload, early enough
 // for their latency to hide behind other work where it can.
+// the Q4 fold on packed f32 ops (A/B: -DQP_FOLD_PK=0)
+#ifndef QP_FOLD_PK
+#define QP_FOLD_PK 1
+#endif
+
 template <int WT, int NW, int BM, int NTW, int KBT = KB>
 struct MainloopPre {
     static constexpr int IT = (BM * (2 * KBT) + NW * 64 - 1) / (NW * 64);
@@ -674,6 +679,24 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                         if (rt * NTW == t + 2) lds_a(rt);
                     if (t + 1 < T) blk[(t + 1) & 1] = blk_of((t + 1) / NTW, (t + 1) % NTW);
                     const int rt = t / NTW, nt = t % NTW;
+                    if constexpr (QN && QP_FOLD_PK) {
+                    // nibble weights: the fold on packed f32 (v_pk_mul / v_pk_fma; the
+                    // same per-element roundings as the scalar fold).  C5 A/B: 3-8 %
+                    // faster for W_Q4_1N, 7-12 % slower for the split planes.
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        float2v v = {acc[rt][nt][2 * h], acc[rt][nt][2 * h + 1]};
+                        float2v sc2 = TRANS ? float2v{da[rt][0], da[rt][0]} : float2v{da[rt][2 * h], da[rt][2 * h + 1]};
+                        if constexpr (QN)
+                            sc2 = sc2 * (TRANS ? float2v{dw[nt][2 * h], dw[nt][2 * h + 1]} : float2v{dw[nt][0], dw[nt][0]});
+                        v = __builtin_elementwise_fma(sc2, float2v{blk[t & 1][2 * h], blk[t & 1][2 * h + 1]}, v);
+                        if constexpr (QN1)  // + m_w s_a
+                            v = __builtin_elementwise_fma(float2v{dw[nt][1], dw[nt][1]}, float2v{sa[rt][2 * h], sa[rt][2 * h + 1]}, v);
+                        asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
+                        acc[rt][nt][2 * h] = v[0];
+                        acc[rt][nt][2 * h + 1] = v[1];
+                    }
+                    } else {
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         float v = acc[rt][nt][i];
@@ -683,6 +706,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                         if constexpr (QN1) v = __builtin_fmaf(dw[nt][1], sa[rt][i], v);  // + m_w s_a
                         asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
                         acc[rt][nt][i] = v;
+                    }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
