@@ -44,6 +44,12 @@ typedef int int16v __attribute__((ext_vector_type(16)));
 #define I8_UP_T 2
 #endif
 
+// development ablations (tools/f6_abl_libs.sh builds variants): bit 0 = no
+// weight loads in the main loop
+#ifndef I8_ABL
+#define I8_ABL 0
+#endif
+
 constexpr int I8_KC = 128;          // K per LDS chunk: 4 quant blocks (one scale vector)
 constexpr int I8_LDQ = I8_KC + 16;  // token row stride of the LDS chunk, bytes: ds_read_b128 conflict-free
 
@@ -176,6 +182,9 @@ struct I8Pipe {
     // block b - nkb of the next tile at ft0n) into ring slot S
     template <int S>
     __device__ __forceinline__ void wload(const GemmArgs &g, int nkb, int ft0, int ft0n, int b) {
+#if I8_ABL & 1
+        if (b >= 2) return;  // ablation (timing only, results wrong): no weight streaming after the prime
+#endif
         const bool nx = b >= nkb;
         const int ft = nx ? ft0n : ft0, bb = nx ? b - nkb : b;
 #pragma unroll

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace bertamd {
 
@@ -522,11 +523,19 @@ __device__ __forceinline__ half8 nib_to_f16(uint32_t x) {
 #define QP_FOLD_PK 1
 #endif
 
+// W blocks in flight in the main loop's register ring: 2 (split planes, F16),
+// QN_RING for nibble records (a quarter of the bytes, half the MFMAs per
+// block: the loads need more blocks of cover)
+#ifndef QN_RING
+#define QN_RING 4
+#endif
+constexpr int w_ring(int wt) { return wt == W_F32 ? 1 : (wt == W_Q4_0N || wt == W_Q4_1N) ? QN_RING : 2; }
+
 template <int WT, int NW, int BM, int NTW, int KBT = KB>
 struct MainloopPre {
     static constexpr int IT = (BM * (2 * KBT) + NW * 64 - 1) / (NW * 64);
     AReg<act_of(WT)> ar[IT];
-    WFrag<WT> wf[WT == W_F32 ? 1 : 2][NTW];
+    WFrag<WT> wf[w_ring(WT)][NTW];
 };
 
 template <int WT, int NW, int BM, int NTW, int KBT = KB>
@@ -546,7 +555,7 @@ __device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW, KB
     }
     if constexpr (WT != W_F32) {
 #pragma unroll
-        for (int kb = 0; kb < 2; kb++)
+        for (int kb = 0; kb < w_ring(WT); kb++)  // K >= 32 * w_ring(WT): launch_gemm / launch_qkv_attention
 #pragma unroll
             for (int nt = 0; nt < NTW; nt++) pre.wf[kb][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kb);
     }
@@ -586,19 +595,23 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
         asm volatile("" : "+v"(item));
         if (item < ITEMS) a_store<AT, BM, LDA_H, KBT, QN1>(pre.ar[it], smem, item, unscale);
     }
-    // W fragments of the two blocks in flight: block b lives in wf[b & 1] and
-    // is replaced by block b + 2 as soon as its MFMAs are issued
-    WFrag<WT> wf[F32P ? 1 : 2][NTW];
+    // W fragments of the WR blocks in flight: block b lives in wf[b % WR] and
+    // is replaced by block b + WR as soon as its MFMAs are issued; the chunk
+    // loop runs CPR chunks per ring turn so that every slot index is static
+    constexpr int WR = w_ring(WT), CPR = WR > KB ? WR / KB : 1;
+    static_assert(F32P || (WR % KB == 0 || KB % WR == 0), "ring vs chunk");
+    WFrag<WT> wf[WR][NTW];
     if constexpr (!F32P) {
 #pragma unroll
-        for (int kb = 0; kb < 2; kb++)
+        for (int kb = 0; kb < WR; kb++)
 #pragma unroll
             for (int nt = 0; nt < NTW; nt++) wf[kb][nt] = pre.wf[kb][nt];
     }
     __syncthreads();
 
     const float4v zero4 = {0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nkc; kc++) {
+    auto chunk = [&](const int kc, auto P) {
+        constexpr int PC = decltype(P)::value;  // chunk index inside the ring turn
         const bool more = kc + 1 < nkc;
         if (more) {
 #pragma unroll
@@ -611,6 +624,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
         const char *abuf = smem + (kc & 1) * A_BUF;
 #pragma unroll
         for (int kb = 0; kb < KB; kb++) {
+            const int SL = (PC * KB + kb) % WR;  // this block's ring slot (static: kb is unrolled)
             if constexpr (QP) {
                 // Per (row tile, n-tile): blk = A.hi + A.lo  (two MFMAs: the exact
                 // d_w-scaled block dot product, f32-accumulated), then ONE fma
@@ -642,7 +656,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 if constexpr (QN1) {  // Q4_1N: q as fp16 integers, d_w and m_w of the lane's column
 #pragma unroll
                     for (int nt = 0; nt < NTW; nt++) {
-                        const u32x2v r = wf[kb & 1][nt].r;
+                        const u32x2v r = wf[SL][nt].r;
                         wn[nt] = nib_to_f16<1024>(r.x);
                         dw[nt][0] = h2f((uint16_t)r.y);
                         dw[nt][1] = h2f((uint16_t)(r.y >> 16));
@@ -650,7 +664,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 } else if constexpr (QN) {
 #pragma unroll
                     for (int nt = 0; nt < NTW; nt++) {
-                        const u32x4v r = wf[kb & 1][nt].r;
+                        const u32x4v r = wf[SL][nt].r;
                         wn[nt] = nib_to_f16(r.x);
                         if constexpr (TRANS)
                             dw[nt] = float4v{h2f((uint16_t)r.y), h2f((uint16_t)(r.y >> 16)), h2f((uint16_t)r.z),
@@ -663,8 +677,8 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                     if constexpr (QN) {
                         return mfma(a[rt_], wn[nt_], zero4);
                     } else {
-                        const float4v b = mfma(a[rt_], wf[kb & 1][nt_].hi, zero4);
-                        return mfma(a[rt_], wf[kb & 1][nt_].lo, b);
+                        const float4v b = mfma(a[rt_], wf[SL][nt_].hi, zero4);
+                        return mfma(a[rt_], wf[SL][nt_].lo, b);
                     }
                 };
 #pragma unroll
@@ -710,10 +724,10 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if (kc * KB + kb + 2 < nkb) {
+                if (kc * KB + kb + WR < nkb) {
 #pragma unroll
                     for (int nt = 0; nt < NTW; nt++)
-                        wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
+                        wf[SL][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + WR);
                 }
             } else if constexpr (WT == W_F16) {
                 half8 a[RT];
@@ -724,11 +738,11 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 for (int nt = 0; nt < NTW; nt++)
 #pragma unroll
                     for (int rt = 0; rt < RT; rt++)
-                        acc[rt][nt] = TRANS ? __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[kb & 1][nt].h, a[rt], acc[rt][nt], 0, 0, 0)
-                                            : __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[kb & 1][nt].h, acc[rt][nt], 0, 0, 0);
-                if (kc * KB + kb + 2 < nkb) {
+                        acc[rt][nt] = TRANS ? __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[SL][nt].h, a[rt], acc[rt][nt], 0, 0, 0)
+                                            : __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], wf[SL][nt].h, acc[rt][nt], 0, 0, 0);
+                if (kc * KB + kb + WR < nkb) {
 #pragma unroll
-                    for (int nt = 0; nt < NTW; nt++) wf[kb & 1][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + 2);
+                    for (int nt = 0; nt < NTW; nt++) wf[SL][nt] = w_load<WT>(args.W, (ntile0 + nt) * nkb + kc * KB + kb + WR);
                 }
             } else {
 #pragma unroll
@@ -760,8 +774,14 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
             }
         }
         __syncthreads();
+    };
+    for (int kc = 0; kc < nkc; kc += CPR) {
+        chunk(kc, std::integral_constant<int, 0>{});
+        if constexpr (CPR > 1) {
+            static_assert(CPR == 2, "two chunks per ring turn");
+            if (kc + 1 < nkc) chunk(kc + 1, std::integral_constant<int, 1>{});
+        }
     }
-
 }
 
 template <int WT, int EPI, int BN, int NW, int BM>
@@ -1652,7 +1672,9 @@ hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a,
         case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, s);
         case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, s);
         case W_Q4_0D: return qkv_attn_w<W_Q4_0, W_Q4_0D>(g, a, n_blocks, s);
-        case W_Q4_0N: return qkv_attn_w<W_Q4_0N, W_Q4_0>(g, a, n_blocks, s);
+        case W_Q4_0N:
+            if (g.K < 32 * w_ring(W_Q4_0N)) return hipErrorInvalidValue;
+            return qkv_attn_w<W_Q4_0N, W_Q4_0>(g, a, n_blocks, s);
         case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, s);
     }
     return hipErrorInvalidValue;
@@ -1919,6 +1941,7 @@ static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
 template <int WT>
 static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
     if constexpr (WT == W_Q4_0N || WT == W_Q4_1N) {  // nibble weights: QKV (unfused), O / down (+ LN or residual)
+        if (a.K < 32 * w_ring(WT)) return hipErrorInvalidValue;  // the ring's preload reads w_ring blocks
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_LN && a.N == 384)
             return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
