@@ -34,6 +34,8 @@ SEED = 20250117
 METRIC = "embeddings/sec at seq_len=128 batch=1024; cosine-sim vs ggml CPU ref"
 PEAK_FP16_TFLOPS = 2516.6  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFLOPS = 157.3
+PEAK_INT8_TOPS = 2 * PEAK_FP16_TFLOPS  # i8 MFMA: 2x the bf16 rate per clock (MI355X_MICROARCH.md MFMA table)
+I8_KERNELS = ("gemm_up_gelu", "gemm_down_ln", "gemm_ffn_ln")  # the int8-MFMA GEMMs of the Q4 models
 PEAK_HBM_GBS = 8000.0
 
 
@@ -84,6 +86,7 @@ def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
         "gemm_o_ln": 2.0 * M * E * E,
         "gemm_up_gelu": 2.0 * M * E * I,
         "gemm_down_ln": 2.0 * M * I * E,
+        "gemm_ffn_ln": 4.0 * M * E * I,
         "attention": 4.0 * B * N * N * E,
         "qkv_attention": 2.0 * M * E * 3 * E + 4.0 * B * N * N * E,
     }.get(name, 0.0)
@@ -100,6 +103,7 @@ def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
         "gemm_o_ln": M * E * act + E * E * wb + 2 * M * E * 4 + M * E * act,
         "gemm_up_gelu": M * E * act + E * I * wb + M * I * act,
         "gemm_down_ln": M * I * act + E * I * wb + 2 * M * E * 4 + M * E * act,
+        "gemm_ffn_ln": M * E * act + 2 * E * I * wb + 2 * M * E * 4 + M * E * act,  # U stays on chip
         "attention": M * 3 * E * 4 + M * E * act,
         "qkv_attention": M * E * act + 3 * E * E * wb + M * E * act,
         "embed_ln": M * 4 + M * E * (4 + act) + M * E * 4,  # f32 word rows (pos/type tables stay cached)
@@ -132,7 +136,7 @@ def pmc_traffic(csv_path: str, kernel_substr: str):
 # name fragments of the dominant kernels' mangled symbols (for PMC CSV lookup)
 KERNEL_SYMBOL = {
     "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "i8_up_gelu_kernel",
-    "gemm_down_ln": "i8_ln384_kernel", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
+    "gemm_down_ln": "i8_ln384_kernel", "gemm_ffn_ln": "i8_ffn384_kernel", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
     "pool_l2": "pool_l2_kernel",
 }
 
@@ -332,9 +336,12 @@ def main():
         fl = kernel_flops(dominant, B, N, hp)
         if fl:
             peak = PEAK_FP32_MFMA_TFLOPS if (args.ftype == "f32" and dominant != "attention") else PEAK_FP16_TFLOPS
+            pdt = "fp32" if args.ftype == "f32" and dominant != "attention" else "fp16"
+            if args.ftype in ("q4_0", "q4_1") and dominant in I8_KERNELS:
+                peak, pdt = PEAK_INT8_TOPS, "int8"  # priced against the int8 MFMA it runs on
             ach = fl / avg_s / 1e12
             roofline = dict(kernel=dominant, bound="mfma", achieved=round(ach, 1), peak=peak, unit="TFLOP/s",
-                            frac=round(ach / peak, 4), flops_per_launch=fl)
+                            frac=round(ach / peak, 4), flops_per_launch=fl, peak_dtype=pdt)
         else:
             by = kernel_bytes(dominant, B, N, hp, args.ftype)
             ach = by / avg_s / 1e9

@@ -213,6 +213,13 @@ bool gemm_gelu_blk8(int wtype);
 // EPI_LN (N == 384), EPI_RESID (N % 256 == 0); K % 128 == 0; Mpad % 128 == 0.
 bool i8_gemm_supported(int epi, int N, int K);
 hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
+// The whole FFN of an n_embd 384 layer in one kernel (gemm_i8.hip
+// i8_ffn384_kernel): u = the FFN-up GemmArgs (A = Xa, bias, gelu pair view, and
+// in Wi the weight stream of both projections, runtime.cpp upload_ffn_i8),
+// d = the FFN-down + LN GemmArgs (Wi, bias, X, ln_w / ln_b, eps, out_act);
+// u.A and d.out_act may be the same buffer.  I % 384 == 0; Mpad % 64 == 0.
+bool i8_ffn_supported(int E, int I);
+hipError_t launch_ffn_i8(int wtype, const GemmArgs &u, const GemmArgs &d, int Mpad, hipStream_t s);
 
 // Q4_0 x Q8D GEMMs on the fp6 MFMA (gemm_f6.hip): A in Q8D; EPI_GELU_ACT
 // (N % 512 == 0, output Q8D), EPI_LN (N == 384, output `out_type` W_Q4_0D or

@@ -176,6 +176,7 @@ struct DevMat {
 struct DevLayer {
     WPtr qkv, o, up, down;
     I8W o8, up8, down8;  // Q4 weights for the int8-MFMA GEMMs (gemm_i8.hip)
+    I8W ffn8;            // both FFN projections as the fused kernel's stream (upload_ffn_i8)
     F6W o6, up6, down6;  // Q4_0 weights for the fp6-MFMA GEMMs (gemm_f6.hip)
     WPtr qkv_plain;  // head-major QKV in grouped, plain tile order: qkv_attention_kernel's copy (when supported)
     float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
@@ -264,6 +265,9 @@ struct bert_ctx {
     // Q4_0 QKV (fused and unfused) and split-path O weights as nibbles,
     // dequantised inside the fp16 MFMA GEMM (kernels.h W_Q4_0N); nib_select
     bool q4nib = false;
+    // FFN-up + GELU + FFN-down + LN in one kernel (gemm_i8.hip i8_ffn384_kernel;
+    // ffn_select): ffn_ok = its weight stream is uploaded, ffn_fused = in use
+    bool ffn_ok = false, ffn_fused = false;
     // run_pipeline knobs, read from the environment once at load
     // (BERT_AMD_SPLIT, BERT_AMD_PACK) and changed only by bert_amd_set_option:
     // two row groups on two streams (default on); fused-tile packing
@@ -442,28 +446,30 @@ Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_
     return p;
 }
 
-// Repack a Q4_0 / Q4_1 [N][K] matrix for the int8-MFMA GEMMs (kernels.h
-// I8W): nibbles expanded to int8 (q - 8 for Q4_0, q for Q4_1) in fragment
-// order, the fp16 block scales (and Q4_1 minima) widened to f32 vectors.
-// Weight row m of each 32-row tile holds feature perm(m), so that a lane of
-// the 32x32 MFMA result holds 16 consecutive output features.
-bool upload_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vector<const uint8_t *> &rows,
-               int64_t K) {
+struct I8Host {
+    std::vector<int8_t> q;
+    std::vector<float> d, m;
+    std::vector<uint16_t> dh;
+};
+
+I8Host repack_i8(uint32_t type, const std::vector<const uint8_t *> &rows, int64_t K) {
     const int64_t N = (int64_t)rows.size(), nkb = K / 32, nft = N / 32;
     const bool q1 = type == GT_Q4_1;
     const int bs = q1 ? 20 : 18, qoff = q1 ? 4 : 2;
     auto perm = [](int m) { return 16 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3); };
-    std::vector<int8_t> q((size_t)(N * K));
-    std::vector<float> d((size_t)(N * nkb)), mv(q1 ? (size_t)(N * nkb) : 0);
-    std::vector<uint16_t> dhv(q1 ? 0 : (size_t)(N * nkb));
+    I8Host h;
+    h.q.resize((size_t)(N * K));
+    h.d.resize((size_t)(N * nkb));
+    h.m.resize(q1 ? (size_t)(N * nkb) : 0);
+    h.dh.resize(q1 ? 0 : (size_t)(N * nkb));
     for (int64_t ft = 0; ft < nft; ft++)
         for (int64_t b = 0; b < nkb; b++)
             for (int lane = 0; lane < 64; lane++) {
-                const int mrow = lane & 31, h = lane >> 5;
+                const int mrow = lane & 31, hf = lane >> 5;
                 const uint8_t *blk = rows[(size_t)(32 * ft + perm(mrow))] + b * bs;
-                int8_t *dst = &q[(size_t)(((ft * nkb + b) * 64 + lane) * 16)];
+                int8_t *dst = &h.q[(size_t)(((ft * nkb + b) * 64 + lane) * 16)];
                 for (int j = 0; j < 16; j++) {
-                    const int e = 16 * h + j;
+                    const int e = 16 * hf + j;
                     const uint8_t byte = blk[qoff + (e & 15)];
                     const int v = e < 16 ? (byte & 15) : (byte >> 4);
                     dst[j] = (int8_t)(q1 ? v : v - 8);
@@ -477,22 +483,73 @@ bool upload_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vec
                     uint16_t dh, mh;
                     std::memcpy(&dh, blk, 2);
                     const size_t at = (size_t)(((ft * (nkb / 4) + g) * 32 + mrow) * 4 + jj);
-                    d[at] = f16_to_f32(dh);
-                    if (!q1) dhv[at] = dh;
+                    h.d[at] = f16_to_f32(dh);
+                    if (!q1) h.dh[at] = dh;
                     if (q1) {
                         std::memcpy(&mh, blk + 2, 2);
-                        mv[at] = f16_to_f32(mh);
+                        h.m[at] = f16_to_f32(mh);
                     }
                 }
+    return h;
+}
+
+bool upload_i8w(std::vector<void *> &track, I8W &w, const I8Host &h) {
     void *pq = nullptr, *pd = nullptr, *pm = nullptr, *ph = nullptr;
-    if (!upload(track, &pq, q.data(), q.size()) || !upload(track, &pd, d.data(), d.size() * 4)) return false;
-    if (q1 && !upload(track, &pm, mv.data(), mv.size() * 4)) return false;
-    if (!q1 && !upload(track, &ph, dhv.data(), dhv.size() * 2)) return false;
+    if (!upload(track, &pq, h.q.data(), h.q.size()) || !upload(track, &pd, h.d.data(), h.d.size() * 4)) return false;
+    if (!h.m.empty() && !upload(track, &pm, h.m.data(), h.m.size() * 4)) return false;
+    if (!h.dh.empty() && !upload(track, &ph, h.dh.data(), h.dh.size() * 2)) return false;
     w.q = (const int8_t *)pq;
     w.d = (const float *)pd;
     w.m = (const float *)pm;
     w.dh = (const uint16_t *)ph;
     return true;
+}
+
+// Repack a Q4_0 / Q4_1 [N][K] matrix for the int8-MFMA GEMMs (kernels.h
+// I8W): nibbles expanded to int8 (q - 8 for Q4_0, q for Q4_1) in fragment
+// order, the fp16 block scales (and Q4_1 minima) widened to f32 vectors.
+// Weight row m of each 32-row tile holds feature perm(m), so that a lane of
+// the 32x32 MFMA result holds 16 consecutive output features.
+bool upload_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vector<const uint8_t *> &rows,
+               int64_t K) {
+    return upload_i8w(track, w, repack_i8(type, rows, K));
+}
+
+// The fused FFN kernel's weight stream (gemm_i8.hip i8_ffn384_kernel): for
+// each of the 12 waves, the int8 fragments of the blocks it reads in its
+// per-tile order (slices j = 0 .. I/384 - 1: up_j = 12 blocks of up f-tile
+// 12 j + w, then down_j = blocks 12 j .. 12 j + 11 of down f-tile w),
+// contiguous, and the chunk scale vectors (4 blocks) in the same order — the
+// same values as upload_i8's, so the kernel's loads are linear in the sequence.
+bool upload_ffn_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vector<const uint8_t *> &up_rows,
+                   const std::vector<const uint8_t *> &down_rows, int64_t E, int64_t I) {
+    const I8Host U = repack_i8(type, up_rows, E), D = repack_i8(type, down_rows, I);
+    const int64_t nj = I / 384, qt = 24 * nj, ct = 6 * nj, nkbu = E / 32, nkbd = I / 32;
+    const bool q1 = type == GT_Q4_1;
+    I8Host S;
+    S.q.resize((size_t)(12 * qt * 64 * 16));
+    S.d.resize((size_t)(12 * ct * 32 * 4));
+    if (q1) S.m.resize(S.d.size());
+    else S.dh.resize(S.d.size());
+    for (int64_t wv = 0; wv < 12; wv++) {
+        for (int64_t q = 0; q < qt; q++) {
+            const int64_t p = q / 12, b = q % 12, j = p / 2;
+            const int8_t *src = (p & 1) ? &D.q[(size_t)((wv * nkbd + 12 * j + b) * 64 * 16)]
+                                        : &U.q[(size_t)(((12 * j + wv) * nkbu + b) * 64 * 16)];
+            std::memcpy(&S.q[(size_t)((wv * qt + q) * 64 * 16)], src, 64 * 16);
+        }
+        for (int64_t c = 0; c < ct; c++) {
+            const int64_t p = c / 3, cc = c % 3, j = p / 2;
+            const bool dn = p & 1;
+            const I8Host &H = dn ? D : U;
+            const size_t at = (size_t)((dn ? wv * (nkbd / 4) + 3 * j + cc : (12 * j + wv) * (nkbu / 4) + cc) * 32 * 4);
+            const size_t to = (size_t)((wv * ct + c) * 32 * 4);
+            std::memcpy(&S.d[to], &H.d[at], 32 * 4 * 4);
+            if (q1) std::memcpy(&S.m[to], &H.m[at], 32 * 4 * 4);
+            else std::memcpy(&S.dh[to], &H.dh[at], 32 * 4 * 2);
+        }
+    }
+    return upload_i8w(track, w, S);
 }
 
 // Repack a Q4_0 [N][K] matrix for the fp6-MFMA GEMMs (kernels.h F6W): per
@@ -720,6 +777,16 @@ void f6_select(bert_ctx *ctx) {
     if (ctx->f6) ctx->i8_o = ctx->i8_up = ctx->i8_down = false;
 }
 
+// The fused FFN kernel (gemm_i8.hip i8_ffn384_kernel) where the int8 FFN-up and
+// FFN-down + LN kernels run: n_embd 384, I % 384 == 0.  Opt-in (bitwise the
+// two-kernel path, 5 % slower on the headline batch): env
+// BERT_AMD_FFN=1 (read at load) or bert_amd_set_option "ffn_fused".
+void ffn_select(bert_ctx *ctx) {
+    const char *e = std::getenv("BERT_AMD_FFN");
+    ctx->ffn_ok = ctx->i8_up && ctx->i8_down && !ctx->f6 && i8_ffn_supported(ctx->hp.n_embd, ctx->hp.n_intermediate);
+    ctx->ffn_fused = ctx->ffn_ok && e && e[0] == '1';
+}
+
 // Q4 weights as nibbles with in-kernel dequant (kernels.h W_Q4_0N / W_Q4_1N):
 // env BERT_AMD_Q4NIB=1 (read at load).  Q4_0 (n_embd 384): the QKV (fused and
 // unfused) and O weights; not with the fp6 path, whose fused kernel stores a
@@ -862,13 +929,6 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
         u.gelu.n_pad = (int)tables().gelu_pair.size();  // the pair view (kernels.hip gelu_lookup)
         u.gelu.cap = tables().gelu_cap;
-        if (ctx->i8_up) {
-            u.Wi = L.up8;
-            LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt, EPI_GELU_ACT, u, (int)rows, st));
-        } else {
-            LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)rows, st));
-        }
-
         GemmArgs dn;
         dn.A = Ua;
         dn.K = I;
@@ -880,6 +940,18 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         dn.ln_w = L.ln2_w;
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
+        if (ctx->ffn_fused) {  // U stays in the workgroup: Ua is not touched
+            u.Wi = L.ffn8;
+            LAUNCH_OK("gemm_ffn_ln", launch_ffn_i8(wt, u, dn, (int)rows, st));
+            return true;
+        }
+        if (ctx->i8_up) {
+            u.Wi = L.up8;
+            LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt, EPI_GELU_ACT, u, (int)rows, st));
+        } else {
+            LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)rows, st));
+        }
+
         if (ctx->i8_down) {
             dn.Wi = L.down8;
             if (E == 384) {
@@ -1198,6 +1270,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
             !(ctx->i8_down ? upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I)
                            : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I, down_wtype(ctx) == W_Q4_1N))))
             return false;
+        if (ctx->ffn_ok && !upload_ffn_i8(tr, dl.ffn8, wt, rows_of(l.i_w), rows_of(l.o2_w), E, I)) return false;
         if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
             !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||
             !upload(tr, &dl.ln1_w, l.ln1_w->data, E * 4) || !upload(tr, &dl.ln1_b, l.ln1_b->data, E * 4) ||
@@ -1370,6 +1443,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     i8_select(ctx.get());
     f6_select(ctx.get());
     nib_select(ctx.get());
+    ffn_select(ctx.get());
     if (const char *e = std::getenv("BERT_AMD_SPLIT")) ctx->split = e[0] != '0';
     if (const char *e = std::getenv("BERT_AMD_PACK")) ctx->pack = e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
     if (const char *e = std::getenv("BERT_AMD_FUSE_MIN")) ctx->fuse_min = std::max(0, std::atoi(e));
@@ -2026,6 +2100,12 @@ int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
             return -2;
         }
         ctx->encode_lanes = value;
+    } else if (k == "ffn_fused") {
+        if (value != 0 && !ctx->ffn_ok) {
+            set_err("bert_amd_set_option: ffn_fused needs an n_embd 384 Q4 model on the int8 FFN kernels");
+            return -2;
+        }
+        ctx->ffn_fused = value != 0;
     } else if (k == "fuse_min") {
         if (value < 0) {
             set_err("bert_amd_set_option: fuse_min must be >= 0");

@@ -160,6 +160,29 @@ def test_q4_nibble_qkv_o_golden(case, model_dir, monkeypatch):
     assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
 
 
+@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01", "minilm_q4_1"])
+def test_fused_ffn_bitwise_split(case, model_dir):
+    """FFN-up + GELU + FFN-down + LN in one kernel (gemm_i8.hip
+    i8_ffn384_kernel, the intermediate kept in LDS slice by slice): bitwise the
+    two-kernel int8 path (same block sums, GELU table, Q8 quantiser and
+    block order), and the golden fixtures within the bound."""
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    m = bertlib.BertModel(p)
+    try:
+        m.set_option("ffn_fused", 1)
+        fused = m.eval_batch(toks)
+        assert np.array_equal(fused, m.eval_batch(toks))
+        m.set_option("ffn_fused", 0)
+        split = m.eval_batch(toks)
+    finally:
+        m.close()
+    assert np.array_equal(fused, split), np.abs(fused - split).max()
+    c = cos(fused, want)
+    print(f"fused FFN {case}: 1-cos max {1 - c.min():.2e}")
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
+
+
 @pytest.mark.parametrize("case", ["c5_bge_q4_1_l2", "c5_bge_q4_1_l2_short", "minilm_q4_1"])
 def test_q4_1_nibble_golden(case, model_dir, monkeypatch):
     """Q4_1 unfused-QKV, split O and FFN-down weights as ggml nibbles (env

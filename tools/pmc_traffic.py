@@ -17,6 +17,7 @@ NAMES = {
     # default C3 build: o-proj on the split-fp16 LN GEMM, down on the int8 one
     "gemm_o_ln": ["gemm_kernelILi2ELi2", "gemm_kernel<2, 2,", "i8_ln384_kernel"],
     "gemm_down_ln": ["i8_ln384_kernel", "gemm_kernelILi2ELi2", "gemm_kernel<2, 2,"],
+    "gemm_ffn_ln": ["i8_ffn384_kernel"],
     "embed_ln": ["embed_ln_kernel"],
     "pool_l2": ["pool_l2_kernel"],
 }
