@@ -43,6 +43,11 @@ typedef int int16v __attribute__((ext_vector_type(16)));
 #ifndef I8_UP_T
 #define I8_UP_T 2
 #endif
+// FFN-up output tile staged through LDS for coalesced stores (A/B: measured
+// 284 vs 279-281 µs unstaged on the headline batch, so off; -DI8_UP_STAGE=1)
+#ifndef I8_UP_STAGE
+#define I8_UP_STAGE 0
+#endif
 
 // development ablations (tools/f6_abl_libs.sh builds variants; timing only,
 // results wrong): bit 0 = no weight loads in the main loop; fused FFN: bit 1 =
@@ -375,6 +380,35 @@ __device__ __forceinline__ void i8_store_q8_half(const ActPtr &out, int64_t ld, 
     }
 }
 
+// The same quantiser into a row-major LDS stage of an output tile: q bytes at
+// qst[r * ldq + 32 blk + 16 hh ..], the block scale at dst[r * nblk + blk]
+// (fp16 for Q8_0, f32 for Q8_1).
+template <int WT>
+__device__ __forceinline__ void i8_q8_half_stage(char *qst, int ldq, void *dst, int nblk, int r, int blk, int hh,
+                                                 const float (&y)[16]) {
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; i++) amax = fmaxf(amax, fabsf(y[i]));
+    {
+        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+    }
+    float d, id;
+    q8_scales(amax, d, id);
+    uint4 pk;
+    pk.x = q8_pack4(y[0], y[1], y[2], y[3], id);
+    pk.y = q8_pack4(y[4], y[5], y[6], y[7], id);
+    pk.z = q8_pack4(y[8], y[9], y[10], y[11], id);
+    pk.w = q8_pack4(y[12], y[13], y[14], y[15], id);
+    *(uint4 *)(qst + r * ldq + 32 * blk + 16 * hh) = pk;
+    if (hh == 0) {
+        if constexpr (WT == W_Q4_0)
+            ((uint16_t *)dst)[r * nblk + blk] = f2h(d);
+        else
+            ((float *)dst)[r * nblk + blk] = d;
+    }
+}
+
 // XCD-aware tile order (as gemm_kernel): linear ids are dealt round-robin over
 // the 8 XCDs; each XCD walks a contiguous range, n fastest.
 __device__ __forceinline__ int xcd_linear(int orig, int nwg) {
@@ -395,6 +429,14 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
     using C = I8Chunk<BM, WT == W_Q4_1>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ __attribute__((aligned(16))) uint16_t gtab[GELU_FLAT_LDS];
+#if I8_UP_STAGE
+    // the output tile (Q8 bytes and block scales) staged for coalesced stores:
+    // whole 16-byte pieces of consecutive columns by consecutive threads instead
+    // of each lane's 16 bytes of its own row
+    constexpr int LDU = BN + (WT == W_Q4_1 ? 0 : 16), NBLK = BN / 32, DS = WT == W_Q4_1 ? 4 : 2;
+    __shared__ __attribute__((aligned(16))) char ust[BM * LDU];
+    __shared__ __attribute__((aligned(16))) char dst_[BM * NBLK * DS];
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int nflat8 = (0x8000 + g.gelu.neg_n + 1 + 7) / 8;
     for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)g.gelu.full)[i];
@@ -438,9 +480,31 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
                 float y[16];
 #pragma unroll
                 for (int i = 0; i < 16; i++) y[i] = h2f(gtab[f2h(fmaxf(bias[i] + acc[f][t][i], xlo))]);
+#if I8_UP_STAGE
+                i8_q8_half_stage<WT>(ust, LDU, dst_, NBLK, 32 * (tw + t) + l32, fw + f, hh, y);
+#else
                 i8_store_q8_half<WT>(g.out_act, g.N, mc + 32 * (tw + t) + l32, fc + f, hh, y);
+#endif
             }
         }
+#if I8_UP_STAGE
+        __syncthreads();
+        {
+            // q: BM rows x BN bytes; d: BM rows x NBLK scales (row-contiguous in U)
+            const int64_t col0 = 32 * (int64_t)(fc - fw);
+#pragma unroll
+            for (int k = 0; k < BM * BN / 16 / NT; k++) {
+                const int i = tid + NT * k, r = i / (BN / 16), c = i - r * (BN / 16);
+                *(uint4 *)((int8_t *)g.out_act.q + (mc + r) * g.N + col0 + 16 * c) = *(const uint4 *)(ust + r * LDU + 16 * c);
+            }
+            constexpr int DPR = NBLK * DS / 16;  // 16-byte pieces of scales per row
+            if (tid < BM * DPR) {
+                const int r = tid / DPR, c = tid - r * DPR;
+                *(uint4 *)((char *)g.out_act.d + ((mc + r) * (g.N / 32) + (fc - fw)) * DS + 16 * c) =
+                    *(const uint4 *)(dst_ + (r * NBLK) * DS + 16 * c);
+            }
+        }
+#endif
     }
 }
 
