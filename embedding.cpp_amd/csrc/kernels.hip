@@ -1360,6 +1360,15 @@ constexpr int QKVA_NW = 12;  // waves
 #ifndef QKVA_KB
 #define QKVA_KB 2  // 32-wide blocks per main-loop chunk in the fused kernel
 #endif
+// A/B (-DQKVA_KEEP_S=1): the fused kernel's attention keeps its (<= 4) score
+// tiles in registers between the max pass and the probability pass instead of
+// recomputing them.  Measured: with two units per main loop it spills (the
+// second unit's accumulators are live) and runs 360 -> 463 us; with one unit
+// per main loop (BERT_AMD_QKVA_NTW=1) 410 -> 413 us, i.e. the 37.5 % fewer
+// attention MFMAs buy nothing: the attention phase is not MFMA-bound.
+#ifndef QKVA_KEEP_S
+#define QKVA_KEEP_S 0
+#endif
 
 // D: head dim; NTW: 192-feature units per main loop (qkv_attention_ntw); PK:
 // sentence tiles (a.tiles)
@@ -1563,11 +1572,25 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                         return S;
                     };
                     float mx = -INFINITY;
+#if QKVA_KEEP_S
+                    // the key tiles' scores stay in registers for pass 2 (n <= 128: at
+                    // most 4 tiles), so each score tile is computed once
+                    float16v Sk[4];
+#pragma unroll
+                    for (int kt = 0; kt < 4; kt++) {
+                        if (kt < nkt) {
+                            Sk[kt] = scores(kt);
+#pragma unroll
+                            for (int j = 0; j < 16; j++) mx = fmaxf(mx, Sk[kt][j]);
+                        }
+                    }
+#else
                     for (int kt = 0; kt < nkt; kt++) {
                         const float16v S = scores(kt);
 #pragma unroll
                         for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
                     }
+#endif
                     mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
                     // ggml's double sum of the fp16 probabilities, exactly: every p is a
                     // multiple of 2^-24 in [0, 1], so p * 2^24 is an integer and the
@@ -1575,8 +1598,15 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     uint32_t sum = 0;
                     float16v o[1];
                     o[0] = float16v{};
+#if QKVA_KEEP_S
+#pragma unroll
+                    for (int kt = 0; kt < 4; kt++) {
+                        if (kt >= nkt) continue;
+                        const float16v S = Sk[kt];
+#else
                     for (int kt = 0; kt < nkt; kt++) {
                         const float16v S = scores(kt);
+#endif
                         half8 ph[2];
 #pragma unroll
                         for (int j = 0; j < 16; j++) {
