@@ -277,10 +277,14 @@ struct bert_ctx {
     // pair, whose GEMM and attention spread a sentence over many workgroups
     int split = 1, pack = -1, fuse_min = 48;
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
-    // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1):
-    // at most lanes x merge x n_batch_size sentences in flight per device
-    // (batch 16, 4096 texts: 1 x 1 12 k emb/s, 4 x 1 35-56 k, 2 x 4 60 k)
-    int encode_lanes = 2, encode_merge = 4;
+    // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
+    // merging only up to encode_merge_rows sentences (slices that large already
+    // fill the chip alone): at most lanes x max(n_batch_size,
+    // min(merge x n_batch_size, encode_merge_rows)) sentences in flight per
+    // device.  Batch 16, 4096 texts of 8..128 tokens (bench consumer line):
+    // lanes x merge 1 x 1 12 k emb/s, 4 x 1 35-56 k, 2 x 4 101 k, 4 x 4 109 k,
+    // 8 x 4 92 k, 6 x 8 124 k, 4 x 8 173 k, 2 x 16 184 k (device-resident 265 k)
+    int encode_lanes = 2, encode_merge = 16, encode_merge_rows = 256;
     std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
 };
 
@@ -1449,6 +1453,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     if (const char *e = std::getenv("BERT_AMD_FUSE_MIN")) ctx->fuse_min = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("BERT_AMD_ENCODE_LANES")) ctx->encode_lanes = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("BERT_AMD_ENCODE_MERGE")) ctx->encode_merge = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("BERT_AMD_ENCODE_MERGE_ROWS")) ctx->encode_merge_rows = std::max(1, std::atoi(e));
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {
@@ -1637,7 +1642,9 @@ void eval_grouped(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok,
 // the working set stays bounded by lanes x merge x n_batch_size sentences.
 void encode_slices(bert_ctx *ctx, int32_t n, int32_t chunk, bert_vocab_id **toks, int32_t *ntok, float **embs) {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    chunk = (int32_t)std::min<int64_t>(n, (int64_t)chunk * ctx->encode_merge);
+    if (chunk < ctx->encode_merge_rows)
+        chunk = (int32_t)std::min<int64_t>({(int64_t)n, (int64_t)chunk * ctx->encode_merge,
+                                            std::max<int64_t>(chunk, ctx->encode_merge_rows)});
     const int nslice = (n + chunk - 1) / chunk, nr = (int)ctx->reps.size();
     const int nl = std::max(1, std::min(ctx->encode_lanes, (nslice + nr - 1) / nr));
     for (auto &r : ctx->reps) {
@@ -2094,6 +2101,12 @@ int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
             return -2;
         }
         ctx->encode_merge = value;
+    } else if (k == "encode_merge_rows") {
+        if (value < 1) {
+            set_err("bert_amd_set_option: encode_merge_rows must be >= 1");
+            return -2;
+        }
+        ctx->encode_merge_rows = value;
     } else if (k == "encode_lanes") {
         if (value < 1) {
             set_err("bert_amd_set_option: encode_lanes must be >= 1");

@@ -101,10 +101,12 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
                         thread with its own workspace and streams (default 2;
                         BERT_AMD_ENCODE_LANES)
      "encode_merge" n >= 1 bert_encode_batch: consecutive n_batch_size slices a
-                        lane evaluates as one ragged batch (default 4;
-                        BERT_AMD_ENCODE_MERGE; 1 = one slice per GPU batch).
-                        At most lanes x merge x n_batch_size sentences are in
-                        flight per device
+                        lane evaluates as one ragged batch (default 16;
+                        BERT_AMD_ENCODE_MERGE; 1 = one slice per GPU batch),
+                        merged only up to "encode_merge_rows" sentences
+                        (default 256; BERT_AMD_ENCODE_MERGE_ROWS).  At most
+                        lanes x max(n_batch_size, min(merge x n_batch_size,
+                        merge_rows)) sentences are in flight per device
    Results are identical under every setting. */
 BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int32_t value);
 

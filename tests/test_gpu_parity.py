@@ -749,9 +749,11 @@ def test_encode_batch_lanes_bitwise(model_dir):
         rng = np.random.default_rng(11)
         texts = [" ".join(f"w{int(x)}" for x in rng.integers(0, 500, int(k))) for k in rng.integers(1, 120, 300)]
         want = m.eval_batch([m.tokenize(t) for t in texts])
-        for lanes, merge in ((1, 1), (4, 1), (7, 1), (2, 4), (3, 5)):
+        for lanes, merge, rows in ((1, 1, 256), (4, 1, 256), (7, 1, 256), (2, 4, 256), (3, 5, 256), (2, 16, 256),
+                                   (2, 16, 40)):
             m.set_option("encode_lanes", lanes)
             m.set_option("encode_merge", merge)
+            m.set_option("encode_merge_rows", rows)
             assert np.array_equal(m.encode(texts, batch_size=16), want)
         assert np.array_equal(m.encode(texts, batch_size=256), want)
     finally:
