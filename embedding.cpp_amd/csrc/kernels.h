@@ -104,7 +104,9 @@ enum Epi : int {
     EPI_GELU_ACT = 1,  // gelu(b + W.x) in the next matmul's activation format
     EPI_LN = 2,        // LN((b + W.x) + X) -> X and activation format (the workgroup owns whole rows)
     EPI_RESID = 3,     // (b + W.x) + X -> X; LayerNorm then runs in launch_ln (rows too wide for one tile)
-    EPI_NONE = 4       // main-loop probe (tools/gemm_bench): nothing stored
+    EPI_NONE = 4,      // main-loop probe (tools/gemm_bench): nothing stored
+    EPI_RESLN = 5      // EPI_RESID over all of a row tile's column tiles in one workgroup, then
+                       // LayerNorm of its rows -> X and activation format (Q4 weights, N 768 / 1024)
 };
 
 // Piecewise view of a 65536-entry fp16 -> fp16 table (ggml's GELU / exp

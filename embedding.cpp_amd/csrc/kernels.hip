@@ -276,20 +276,24 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
     }
 }
 
-// LayerNorm of X rows in place (+ activation store) for the GEMMs whose rows
-// are too wide for one workgroup (EPI_RESID), same arithmetic as the fused
-// epilogue: 16 rows per workgroup, four lanes per (row, 32-element block).
-template <int WT, int NBLK>
-__global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__restrict__ lnw,
-                                                      const float *__restrict__ lnb, float eps, ActPtr out) {
-    constexpr int E = NBLK * 32, TPT = 64 * NBLK / 256;
-    __shared__ double red1[16 * NBLK], red2[16 * NBLK];
+// LayerNorm of 16 X rows from row0 in place (+ activation store), NT threads,
+// four lanes per (row, 32-element block), TPT tasks per thread; red: 16 * NBLK
+// doubles, stat: 16 floats of LDS (barriers inside; the caller orders the
+// slices).  Statistics as ggml_norm: mean = double sum / E, then the double
+// sum of the f32 squares of (x - mean).  A row's 32-wide block partials are
+// summed in block order by one thread per row (not by every lane of the row),
+// which then writes the row's mean / scale.  Shared by ln_rows_kernel and the
+// GEMM's EPI_RESLN epilogue, so both give the same bits.
+template <int WT, int NBLK, int NT>
+__device__ __forceinline__ void ln_rows16(float *X, const float *__restrict__ lnw, const float *__restrict__ lnb,
+                                          float eps, const ActPtr &out, int64_t row0, double *red, float *stat) {
+    constexpr int E = NBLK * 32, TPT = 64 * NBLK / NT;
+    static_assert(TPT * NT == 64 * NBLK, "whole tasks per thread");
     const int tid = threadIdx.x;
-    const int64_t row0 = (int64_t)blockIdx.x * 16;
     float v[TPT][8];
 #pragma unroll
     for (int it = 0; it < TPT; it++) {
-        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+        const int t = tid + NT * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
         const float4v *xp = (const float4v *)(X + (row0 + r) * (int64_t)E + c);
         const float4v x0 = xp[0], x1 = xp[1];
         double s = 0.0;
@@ -302,16 +306,20 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__r
         for (int j = 0; j < 8; j++) s += (double)v[it][j];
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
-        if (qq == 0) red1[r * NBLK + b] = s;
+        if (qq == 0) red[r * NBLK + b] = s;
+    }
+    __syncthreads();
+    if (tid < 16) {
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < NBLK; k++) tot += red[tid * NBLK + k];
+        stat[tid] = (float)(tot / E);
     }
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < TPT; it++) {
-        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK;
-        double tot = 0.0;
-#pragma unroll
-        for (int k = 0; k < NBLK; k++) tot += red1[r * NBLK + k];
-        const float mean = (float)(tot / E);
+        const int t = tid + NT * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK;
+        const float mean = stat[r];
         double s2 = 0.0;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -320,17 +328,21 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__r
         }
         s2 += __shfl_xor(s2, 1);
         s2 += __shfl_xor(s2, 2);
-        if (qq == 0) red2[r * NBLK + b] = s2;
+        if (qq == 0) red[r * NBLK + b] = s2;  // the row sums were read before the last barrier
+    }
+    __syncthreads();
+    if (tid < 16) {
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < NBLK; k++) tot += red[tid * NBLK + k];
+        const float var = (float)(tot / E);
+        stat[tid] = 1.0f / sqrtf(var + eps);
     }
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < TPT; it++) {
-        const int t = tid + 256 * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
-        double tot = 0.0;
-#pragma unroll
-        for (int k = 0; k < NBLK; k++) tot += red2[r * NBLK + k];
-        const float var = (float)(tot / E);
-        const float scale = 1.0f / sqrtf(var + eps);
+        const int t = tid + NT * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
+        const float scale = stat[r];
         const float4v w0 = *(const float4v *)(lnw + c), w1 = *(const float4v *)(lnw + c + 4);
         const float4v b0 = *(const float4v *)(lnb + c), b1 = *(const float4v *)(lnb + c + 4);
         float y[8];
@@ -344,6 +356,17 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__r
         xo[1] = float4v{y[4], y[5], y[6], y[7]};
         store_act_quarter<WT>(out, E, row0 + r, b, qq, y);
     }
+    __syncthreads();  // stat / red are reused by the next slice
+}
+
+// LayerNorm of X rows in place (+ activation store) after a separate residual
+// GEMM (EPI_RESID): 16 rows per workgroup.
+template <int WT, int NBLK>
+__global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__restrict__ lnw,
+                                                      const float *__restrict__ lnb, float eps, ActPtr out) {
+    __shared__ double red[16 * NBLK];
+    __shared__ float stat[16];
+    ln_rows16<WT, NBLK, 256>(X, lnw, lnb, eps, out, (int64_t)blockIdx.x * 16, red, stat);
 }
 
 // ---------------------------------------------------------------------------
@@ -784,6 +807,28 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     }
 }
 
+// X = (b + W.x) + X for the wave's column pairs (EPI_RESID, EPI_RESLN): lane
+// (g, c16), pair p, row tile rt, i: row m0 + 16 rt + 4 g + i, columns
+// colw + 32 p + {0, 1}
+template <int RT, int NP, int NTW>
+__device__ __forceinline__ void resid_epilogue(const GemmArgs &args, int64_t m0, int colw,
+                                               const float4v (&acc)[RT][NTW]) {
+    const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        const int col = colw + 32 * p;
+        const float2v b = *(const float2v *)(args.bias + col);
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                float2v *xp = (float2v *)(args.X + (m0 + rt * 16 + 4 * g + i) * args.N + col);
+                const float2v x = *xp;
+                *xp = float2v{(b[0] + acc[rt][2 * p][i]) + x[0], (b[1] + acc[rt][2 * p + 1][i]) + x[1]};
+            }
+    }
+}
+
 template <int WT, int EPI, int BN, int NW, int BM>
 __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtiles, int n_ntiles) {
     constexpr int NT = NW * 64;
@@ -802,10 +847,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     // gemm_gelu_blk8), epilogue in registers; otherwise 16-row LDS slices
     constexpr bool GELU_T = (QP || WT == W_F16) && EPI == EPI_GELU_ACT;
     // LN: two 16-row slice buffers (stage + row partials) for BN <= 768
-    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || GELU_T) ? 0 : (EPI == EPI_LN && BN <= 768 ? 2 : 1) * (16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0));
+    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || EPI == EPI_RESLN || GELU_T) ? 0 : (EPI == EPI_LN && BN <= 768 ? 2 : 1) * (16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0));
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
-    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0, "epilogue: whole quarter-tasks per thread");
+    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || EPI == EPI_RESLN || (BN / 32) % NW == 0,
+                  "epilogue: whole quarter-tasks per thread");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     constexpr bool GT_LDS = EPI == EPI_GELU_ACT;
     __shared__ __attribute__((aligned(16))) uint16_t gtab[GT_LDS ? (GELU_T ? GELU_FLAT_LDS : HALF_TABLE_LDS) : 8];
@@ -890,6 +936,38 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         return;
     }
 
+    if constexpr (EPI == EPI_RESLN) {
+        // One workgroup per BM-row tile walks all n_ntiles column tiles:
+        // X = (b + W.x) + X as EPI_RESID, then LayerNorm of the tile's rows in
+        // place from its own just-written X (same CU: the barrier orders the
+        // other waves' stores before the loads) with ln_rows16 — bitwise the
+        // EPI_RESID + launch_ln pair, without the LN pass's re-read of X from
+        // HBM and its launch (rows too wide for one workgroup's tile: n_embd 768
+        // and 1024 on the Q4 split weights).
+        const int64_t mr = (int64_t)blockIdx.x * BM;
+        for (int nt = 0; nt < n_ntiles; nt++) {
+            const int64_t nt0 = ((int64_t)nt * BN + wv * WN) >> 4;
+            float4v acc[RT][NTW];
+            {
+                MainloopPre<WT, NW, BM, NTW> pre;
+                mainloop_preload(pre, args, mr, nt0);
+                gemm_mainloop<WT, NW, BM, NTW, false>(args, mr, nt0, smem, acc, pre);
+            }
+            resid_epilogue<RT, NP>(args, mr, nt * BN + wv * WN + 2 * c16, acc);
+        }
+        __syncthreads();
+        constexpr int LT = act_of(WT);
+        double *red = (double *)smem;
+        float *stat = (float *)(red + 16 * 32);
+        static_assert(16 * 32 * 8 + 16 * 4 <= SMEM, "LN partials fit the A buffers");
+        for (int r16 = 0; r16 < BM; r16 += 16) {
+            if (args.N == 1024)
+                ln_rows16<LT, 32, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, mr + r16, red, stat);
+            else
+                ln_rows16<LT, 24, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, mr + r16, red, stat);
+        }
+        return;
+    }
     int64_t m0;
     int n0;
     tile_of(blockIdx.x, m0, n0);
@@ -933,19 +1011,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
             for (int j = 0; j < NTW; j++) t += acc[rt][j][0] + acc[rt][j][3];
         if (t == 1234.5678f) args.X[tid] = t;
     } else if constexpr (EPI == EPI_RESID) {  // X = (b + W.x) + X, in registers
-#pragma unroll
-        for (int p = 0; p < NP; p++) {
-            const int col = colw + 32 * p;
-            const float2v b = *(const float2v *)(args.bias + col);
-#pragma unroll
-            for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    float2v *xp = (float2v *)(args.X + (m0 + rt * 16 + 4 * g + i) * args.N + col);
-                    const float2v x = *xp;
-                    *xp = float2v{(b[0] + acc[rt][2 * p][i]) + x[0], (b[1] + acc[rt][2 * p + 1][i]) + x[1]};
-                }
-        }
+        resid_epilogue<RT, NP>(args, m0, colw, acc);
     } else if constexpr (EPI == EPI_QKV) {
         // y = b + W.x in f32 (ggml), split hi = fp16(y), lo = fp16(y - hi) for the
         // attention MFMAs.  A column pair lies wholly in Q|K or in V (E % 32 == 0).
@@ -1954,7 +2020,7 @@ static bool ln_half_rows(int Mpad) {
 template <int WT, int EPI, int BN, int NW, int BM>
 static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
     const int mt = Mpad / BM, nt = a.N / BN;
-    int grid = mt * nt;
+    int grid = EPI == EPI_RESLN ? mt : mt * nt;  // EPI_RESLN: a workgroup walks a row tile's n-tiles
     if constexpr ((WT == W_Q4_0 || WT == W_Q4_1 || WT == W_F16) && EPI == EPI_GELU_ACT) {
         // persistent: one workgroup per CU (the GELU table fills the LDS), a multiple of 8
         if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS) return hipErrorInvalidValue;
@@ -1977,6 +2043,7 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
             return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
                                       : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
+        if (epi == EPI_RESLN) return gemm_t<WT, EPI_RESLN, 256, 8, 128>(a, Mpad, s);
     } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_GELU_ACT)  // 12 waves (3 per SIMD) where N allows; the GELU table fills the LDS
@@ -1986,6 +2053,7 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
             return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
                                       : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
+        if (epi == EPI_RESLN) return gemm_t<WT, EPI_RESLN, 256, 8, 128>(a, Mpad, s);
     } else if constexpr (WT == W_F16) {
         // tools/gemm_bench (e5 shapes): 12-wave 384-column tiles win by 1.3-1.8x over
         // 4-6 waves and by 11-14 % over 768 x 64 tiles (qkv 343 us, up+GELU 368 us)
@@ -2026,6 +2094,7 @@ bool gemm_shape_supported(int epi, int N, int K) {
     if (K % KC) return false;
     if (epi == EPI_QKV) return N % 384 == 0;
     if (epi == EPI_GELU_ACT || epi == EPI_RESID) return N % 256 == 0;
+    if (epi == EPI_RESLN) return N == 768 || N == 1024;  // Q4 split / nibble weights only (gemm_w)
     return N == 384 || N == 768 || N == 1024;
 }
 

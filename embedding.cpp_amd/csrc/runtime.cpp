@@ -285,6 +285,13 @@ struct bert_ctx {
     // lanes x merge 1 x 1 12 k emb/s, 4 x 1 35-56 k, 2 x 4 101 k, 4 x 4 109 k,
     // 8 x 4 92 k, 6 x 8 124 k, 4 x 8 173 k, 2 x 16 184 k (device-resident 265 k)
     int encode_lanes = 2, encode_merge = 16, encode_merge_rows = 256;
+    // Q4 models wider than 384 (LN rows wider than one GEMM tile): the O and
+    // FFN-down residual GEMMs can normalise their rows in the same kernel
+    // (EPI_RESLN: one workgroup walks a row tile's column tiles, then LN) instead
+    // of EPI_RESID + launch_ln; bitwise the same.  Opt-in (env BERT_AMD_RESLN=1
+    // or option "resln"): measured slower on C5 (the in-kernel LN
+    // phase is exposed, one 8-wave workgroup per CU).
+    bool resln = false;
     std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
 };
 
@@ -918,6 +925,8 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             }
         } else if (ln_fused) {
             LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_LN, 0, o, (int)rows, st));
+        } else if (ctx->resln) {
+            LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_RESLN, 0, o, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_RESID, 0, o, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
@@ -966,6 +975,8 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             }
         } else if (ln_fused) {
             LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_LN, 0, dn, (int)rows, st));
+        } else if (ctx->resln) {
+            LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_RESLN, 0, dn, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_RESID, 0, dn, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
@@ -1453,6 +1464,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     if (const char *e = std::getenv("BERT_AMD_FUSE_MIN")) ctx->fuse_min = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("BERT_AMD_ENCODE_LANES")) ctx->encode_lanes = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("BERT_AMD_ENCODE_MERGE")) ctx->encode_merge = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("BERT_AMD_RESLN")) ctx->resln = e[0] == '1';
     if (const char *e = std::getenv("BERT_AMD_ENCODE_MERGE_ROWS")) ctx->encode_merge_rows = std::max(1, std::atoi(e));
     // devices
     int n_visible = 0;
@@ -2101,6 +2113,8 @@ int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
             return -2;
         }
         ctx->encode_merge = value;
+    } else if (k == "resln") {
+        ctx->resln = value != 0;
     } else if (k == "encode_merge_rows") {
         if (value < 1) {
             set_err("bert_amd_set_option: encode_merge_rows must be >= 1");

@@ -97,6 +97,9 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
      "fuse_min" n >= 0 batches of fewer than n sentences (default 48) run the
                         unfused QKV GEMM + attention pair instead of the fused
                         kernel (lower latency for small batches)
+     "resln" 0 | 1      Q4 models of n_embd 768 / 1024: LayerNorm inside the O and
+                        FFN-down residual GEMMs (1) instead of a separate pass
+                        (0, default: faster; BERT_AMD_RESLN)
      "encode_lanes" n >= 1 bert_encode_batch: lanes per device, each a host
                         thread with its own workspace and streams (default 2;
                         BERT_AMD_ENCODE_LANES)

@@ -183,6 +183,32 @@ def test_fused_ffn_bitwise_split(case, model_dir):
     assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
 
 
+@pytest.mark.parametrize("case", ["c5_bge_q4_1_l2", "c5_bge_q4_1_l2_short"])
+@pytest.mark.parametrize("nib", ["0", "1"])
+def test_residual_ln_fused_bitwise(case, nib, model_dir, monkeypatch):
+    """n_embd 1024 Q4 (C5, bge-large Q4_1): the O and FFN-down residual GEMMs
+    normalise their rows in the same kernel (kernels.hip EPI_RESLN: one
+    workgroup walks a row tile's column tiles, then ln_rows16 on its own rows)
+    — bitwise the EPI_RESID + launch_ln pair (reference bert.cpp:955-961,
+    985-991), on the split-plane and the nibble (BERT_AMD_Q4NIB=1) weights, on
+    the fused (short) and unfused (512-token) QKV paths; golden within the bound."""
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    monkeypatch.setenv("BERT_AMD_Q4NIB", nib)
+    m = bertlib.BertModel(p)
+    try:
+        m.set_option("resln", 1)
+        fused = m.eval_batch(toks)
+        assert np.array_equal(fused, m.eval_batch(toks))
+        m.set_option("resln", 0)
+        pair = m.eval_batch(toks)
+    finally:
+        m.close()
+    assert np.array_equal(fused, pair), np.abs(fused - pair).max()
+    c = cos(fused, want)
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
+
+
 @pytest.mark.parametrize("case", ["c5_bge_q4_1_l2", "c5_bge_q4_1_l2_short", "minilm_q4_1"])
 def test_q4_1_nibble_golden(case, model_dir, monkeypatch):
     """Q4_1 unfused-QKV, split O and FFN-down weights as ggml nibbles (env
