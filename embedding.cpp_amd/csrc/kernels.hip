@@ -1787,6 +1787,10 @@ hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a,
 // softmax VALU and the chunk loads are amortised over 256 queries.
 constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, queries per workgroup
 
+#ifndef ATTN_LONG_KT_UNROLL
+#define ATTN_LONG_KT_UNROLL(D) ((D) == 64 ? 1 : 4)  // A/B: -D'ATTN_LONG_KT_UNROLL(D)=4' (the round-2 form)
+#endif
+
 template <int WT, int D>
 __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnArgs a) {
     constexpr int NK = 128, KST = D + 8, VST = NK + 4, NT = ATTN_LONG_NW * 64;
@@ -1899,7 +1903,11 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
         if (st + 1 < 2 * nch) fetch(st + 1 < nch ? st + 1 : st + 1 - nch, st + 1 >= nch);
         if (st == nch) mx = fmaxf(mx, __shfl_xor(mx, 32));  // pass 1 complete
         if (!active) continue;
-#pragma unroll
+        // D = 64: the key-tile loop stays rolled — unrolled, the compiler keeps
+        // more tiles' operands live and spilled 80 B/lane at 256 VGPRs (208
+        // VGPRs, no scratch rolled); D = 32 unrolls without spills
+        constexpr int KTU = ATTN_LONG_KT_UNROLL(D);
+#pragma unroll KTU
         for (int kt = 0; kt < NK / 32; kt++) {
             const int k0 = c * NK + 32 * kt;
             if (k0 >= n) continue;
