@@ -1787,6 +1787,11 @@ hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a,
 // softmax VALU and the chunk loads are amortised over 256 queries.
 constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, queries per workgroup
 
+// development ablations (timing only, wrong results): 1 = no K / V global
+// loads (zeros staged), 2 = no pass-1 score tiles
+#ifndef ATTN_LONG_ABL
+#define ATTN_LONG_ABL 0
+#endif
 #ifndef ATTN_LONG_KT_UNROLL
 #define ATTN_LONG_KT_UNROLL(D) ((D) == 64 ? 1 : 4)  // A/B: -D'ATTN_LONG_KT_UNROLL(D)=4' (the round-2 form)
 #endif
@@ -1830,7 +1835,7 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
         for (int i = 0; i < KIT; i++) {
             const int idx = tid + NT * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
             pkh[i] = pkl[i] = uint4{0u, 0u, 0u, 0u};
-            if (kbase + key < n) {
+            if (!(ATTN_LONG_ABL & 1) && kbase + key < n) {
                 const int64_t off = (int64_t)(beg + kbase + key) * E2 + E + h * D + col;
                 pkh[i] = *(const uint4 *)(a.qk_hi + off);
                 pkl[i] = *(const uint4 *)(a.qk_lo + off);
@@ -1842,6 +1847,7 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
             const int idx = tid + NT * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
             const int64_t off = (int64_t)(h * D + d) * a.ldv + beg + kbase + k8;
             pvh[i] = pvl[i] = half8{};
+            if (ATTN_LONG_ABL & 1) continue;
             if (kbase + k8 + 8 <= n && v_aligned) {
                 pvh[i] = *(const half8 *)(a.vt_hi + off);
                 pvl[i] = *(const half8 *)(a.vt_lo + off);
@@ -1911,6 +1917,7 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
         for (int kt = 0; kt < NK / 32; kt++) {
             const int k0 = c * NK + 32 * kt;
             if (k0 >= n) continue;
+            if ((ATTN_LONG_ABL & 2) && !p2) continue;
             float16v S = scores(k0, 32 * kt);
             if (!p2) {  // pass 1: maxima
 #pragma unroll
