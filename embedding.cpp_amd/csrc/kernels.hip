@@ -1435,6 +1435,9 @@ constexpr int QKVA_NW = 12;  // waves
 #ifndef QKVA_KEEP_S
 #define QKVA_KEEP_S 0
 #endif
+// (Software-pipelined score tiles in the attention phase — tile kt + 1's K.Q
+// MFMAs in flight during tile kt's softmax — measured 368 -> 392-399 us with
+// 28 B/lane of spills: not kept.)
 
 // D: head dim; NTW: 192-feature units per main loop (qkv_attention_ntw); PK:
 // sentence tiles (a.tiles)
@@ -1658,6 +1661,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     }
 #endif
                     mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
+                    const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
                     // ggml's double sum of the fp16 probabilities, exactly: every p is a
                     // multiple of 2^-24 in [0, 1], so p * 2^24 is an integer and the
                     // sum of n <= 128 of them fits a uint32
@@ -1675,14 +1679,22 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 #endif
                         half8 ph[2];
 #pragma unroll
-                        for (int j = 0; j < 16; j++) {
+                        for (int j = 0; j < 16; j += 2) {
                             // ggml_scale after K.Q, then p = exp_tab[fp16(s - max)]: s - max <= 0, and
                             // fp16(max - s) is its magnitude exactly (IEEE subtraction is sign-symmetric;
-                            // masked keys: +inf -> the constant-0 entry)
-                            const uint32_t hm = f2h(mx - S[j] * a.scale);
-                            const uint16_t pb = etab[epos + min(hm, (uint32_t)eneg)];
-                            ph[j >> 3][j & 7] = __builtin_bit_cast(_Float16, pb);
-                            sum += (uint32_t)(h2f(pb) * 16777216.0f);
+                            // masked keys: +inf -> the constant-0 entry).  Two scores per packed f32
+                            // op (v_pk_mul / v_pk_add: the same IEEE roundings per element)
+                            const float2v d2 = mx2 - float2v{S[j], S[j + 1]} * sc2;
+                            uint16_t pb[2];
+#pragma unroll
+                            for (int e = 0; e < 2; e++) {
+                                const float de = d2[e];
+                                const uint32_t hm = f2h(de);
+                                pb[e] = etab[epos + min(hm, (uint32_t)eneg)];
+                                ph[(j + e) >> 3][(j + e) & 7] = __builtin_bit_cast(_Float16, pb[e]);
+                            }
+                            const float2v p2 = float2v{h2f(pb[0]), h2f(pb[1])} * float2v{16777216.0f, 16777216.0f};
+                            sum += (uint32_t)p2[0] + (uint32_t)p2[1];
                         }
                         attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph, dh);
                     }
@@ -1882,10 +1894,11 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
     // scaled, masked scores of the 32-key tile starting at absolute key k0
     int lim = n - 4 * hh;
     asm volatile("" : "+v"(lim));
+    // unscaled (ggml_scale after K.Q is applied where the scores are used: pass 1
+    // takes the max of the unscaled scores, exact since x -> fl(x * scale) is
+    // monotonic for scale > 0; pass 2 scales them)
     auto scores = [&](int k0, int kl0) {
         float16v S = attn_qk<D>(Kh, Kl, KST, kl0, r, hh, qh, ql);
-#pragma unroll
-        for (int j = 0; j < 16; j++) S[j] = S[j] * a.scale;  // ggml_scale after K.Q
         if (k0 + 32 > n) {
 #pragma unroll
             for (int j = 0; j < 16; j++)
@@ -1907,29 +1920,39 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
         commit(p2);
         __syncthreads();
         if (st + 1 < 2 * nch) fetch(st + 1 < nch ? st + 1 : st + 1 - nch, st + 1 >= nch);
-        if (st == nch) mx = fmaxf(mx, __shfl_xor(mx, 32));  // pass 1 complete
+        if (st == nch) mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;  // pass 1 complete
         if (!active) continue;
         // D = 64: the key-tile loop stays rolled — unrolled, the compiler keeps
         // more tiles' operands live and spilled 80 B/lane at 256 VGPRs (208
         // VGPRs, no scratch rolled); D = 32 unrolls without spills
+        // (Software-pipelining the score tiles — the next tile's K.Q MFMAs issued
+        // before this tile's softmax — measured 1 - 3 % slower: not kept.)
         constexpr int KTU = ATTN_LONG_KT_UNROLL(D);
+        if ((ATTN_LONG_ABL & 2) && !p2) continue;
 #pragma unroll KTU
         for (int kt = 0; kt < NK / 32; kt++) {
             const int k0 = c * NK + 32 * kt;
             if (k0 >= n) continue;
-            if ((ATTN_LONG_ABL & 2) && !p2) continue;
             float16v S = scores(k0, 32 * kt);
             if (!p2) {  // pass 1: maxima
 #pragma unroll
                 for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
             } else {    // pass 2: p, sum, P.V
                 uint32_t part = 0;  // 16 terms <= 2^24
+                const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    const uint32_t hm = f2h(mx - S[j]);  // |s - max| as fp16; masked -inf -> +inf -> 0
-                    const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
-                    S[j] = p;
-                    part += (uint32_t)(p * 16777216.0f);
+                for (int j = 0; j < 16; j += 2) {
+                    // |s - max| as fp16 (s scaled); masked -inf -> +inf -> 0.  Two scores
+                    // per packed f32 op (the same IEEE roundings per element)
+                    const float2v d2 = mx2 - float2v{S[j], S[j + 1]} * sc2;
+#pragma unroll
+                    for (int e = 0; e < 2; e++) {
+                        const float de = d2[e];
+                        const uint32_t hm = f2h(de);
+                        S[j + e] = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
+                    }
+                    const float2v p2 = float2v{S[j], S[j + 1]} * float2v{16777216.0f, 16777216.0f};
+                    part += (uint32_t)p2[0] + (uint32_t)p2[1];
                 }
                 sum += part;
                 attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
