@@ -46,9 +46,13 @@ def main():
             out["write_bytes"][name] = round(wb)
             out["bytes_per_launch"][name] = round(fb + wb)
     # whole step: every layer kernel launches n_layer (6) times per step, embed and pool once
+    # (gemm_ffn_ln replaces up + down when the fused FFN kernel is on; otherwise absent)
     per_step = {"embed_ln": 1, "pool_l2": 1}
-    if all(k in out["bytes_per_launch"] for k in NAMES):
-        out["bytes_per_step"] = round(sum(b * per_step.get(k, 6) for k, b in out["bytes_per_launch"].items()))
+    bl = out["bytes_per_launch"]
+    step = [k for k in NAMES if k != "gemm_ffn_ln"] if "gemm_ffn_ln" not in bl else \
+        [k for k in NAMES if k not in ("gemm_up_gelu", "gemm_down_ln")]
+    if all(k in bl for k in step):
+        out["bytes_per_step"] = round(sum(bl[k] * per_step.get(k, 6) for k in step))
     with open(sys.argv[4], "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["bytes_per_launch"]))
