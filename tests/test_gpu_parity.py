@@ -481,6 +481,19 @@ def test_encode_batch_slices_sorted_and_bounded(model_dir):
         assert np.array_equal(m.encode(texts, batch_size=0), emb)
     finally:
         m.close()
+    # merged slices: 8-sentence slices merged 4 at a time but capped at
+    # encode_merge_rows = 16 sentences per GPU batch (one lane)
+    m = bertlib.BertModel(p)
+    try:
+        m.set_option("encode_lanes", 1)
+        m.set_option("encode_merge", 4)
+        m.set_option("encode_merge_rows", 16)
+        emb2 = m.encode(texts, batch_size=8)
+        longest16 = sum(sorted(len(i) for i in ids)[-16:])
+        assert 0 < m.workspace_rows() <= (longest16 + 127) // 128 * 128
+        assert np.array_equal(emb2, emb)
+    finally:
+        m.close()
 
 
 def test_mixed_lengths_group_like_separate_batches(model_dir):
