@@ -1805,11 +1805,13 @@ constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, que
 #define ATTN_LONG_ABL 0
 #endif
 #ifndef ATTN_LONG_KT_UNROLL
-#define ATTN_LONG_KT_UNROLL(D) ((D) == 64 ? 1 : 4)  // A/B: -D'ATTN_LONG_KT_UNROLL(D)=4' (the round-2 form)
+#define ATTN_LONG_KT_UNROLL(D) 1  // A/B: -D'ATTN_LONG_KT_UNROLL(D)=4' (the round-2 form)
 #endif
 
 template <int WT, int D>
-__global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnArgs a) {
+// D = 32: two workgroups per CU (78 KiB of LDS each; the register budget
+// capped at 128 for four waves per SIMD) — 423 -> 333 us at MiniLM 512 x 256
+__global__ __launch_bounds__(ATTN_LONG_NW * 64, D == 32 ? 4 : 1) void attention_long_kernel(AttnArgs a) {
     constexpr int NK = 128, KST = D + 8, VST = NK + 4, NT = ATTN_LONG_NW * 64;
     __shared__ __attribute__((aligned(16))) _Float16 Kh[NK * KST], Kl[NK * KST], Vh[D * VST], Vl[D * VST];
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
@@ -1922,9 +1924,10 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64) void attention_long_kernel(AttnA
         if (st + 1 < 2 * nch) fetch(st + 1 < nch ? st + 1 : st + 1 - nch, st + 1 >= nch);
         if (st == nch) mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;  // pass 1 complete
         if (!active) continue;
-        // D = 64: the key-tile loop stays rolled — unrolled, the compiler keeps
-        // more tiles' operands live and spilled 80 B/lane at 256 VGPRs (208
-        // VGPRs, no scratch rolled); D = 32 unrolls without spills
+        // the key-tile loop stays rolled — unrolled, the compiler keeps more
+        // tiles' operands live: at D = 64 it spilled 80 B/lane at 256 VGPRs
+        // (208 VGPRs, no scratch rolled); at D = 32 rolled is what fits the
+        // 128-VGPR budget of two workgroups per CU (20 B/lane of scratch)
         // (Software-pipelining the score tiles — the next tile's K.Q MFMAs issued
         // before this tile's softmax — measured 1 - 3 % slower: not kept.)
         constexpr int KTU = ATTN_LONG_KT_UNROLL(D);
