@@ -10,7 +10,7 @@ SRC := embedding.cpp_amd/csrc
 INC := -Iinclude -I$(SRC)
 HOST_SRCS := gguf_io.cpp quantize.cpp quantize_model.cpp synth.cpp tokenizer.cpp runtime.cpp
 HOST_OBJS := $(addprefix $(BUILD)/obj/,$(HOST_SRCS:.cpp=.o))
-HIP_OBJS := $(BUILD)/obj/kernels.o $(BUILD)/obj/gemm_i8.o $(BUILD)/obj/gemm_f6.o
+HIP_OBJS := $(BUILD)/obj/kernels.o $(BUILD)/obj/gemm_i8.o
 CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
 HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
@@ -85,8 +85,3 @@ $(BUILD)/qkva_time: tools/qkva_time.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SR
 $(BUILD)/pmc_calib: tools/pmc_calib.hip
 	@mkdir -p $(BUILD)
 	$(HIPCC) -O3 --offload-arch=gfx950 $< -o $@
-
-# development harness: the fp6-MFMA GEMMs against the int8 ones (tools/f6_bench.hip; not shipped)
-$(BUILD)/f6_bench: tools/f6_bench.hip $(SRC)/gemm_f6.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
-	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) $< -o $@

@@ -35,7 +35,8 @@ ABI_SYMBOLS = [
 EXT_SYMBOLS = [
     "bert_amd_load", "bert_amd_n_devices", "bert_amd_hparams", "bert_amd_eval_device",
     "bert_amd_profile_enable", "bert_amd_profile_read", "bert_amd_synth_model", "bert_amd_tokenize_json",
-    "bert_amd_debug_embed", "bert_amd_workspace_rows", "bert_amd_last_error",
+    "bert_amd_debug_embed", "bert_amd_workspace_rows", "bert_amd_last_error", "bert_amd_load_opts",
+    "bert_amd_debug_layers", "bert_amd_set_option",
 ]
 
 # model shapes of BASELINE.json's configs
@@ -77,6 +78,8 @@ def lib() -> ctypes.CDLL:
     L.bert_model_quantize.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
     L.bert_amd_load.restype = ctypes.c_void_p
     L.bert_amd_load.argtypes = [ctypes.c_char_p, I_P, ctypes.c_int32]
+    L.bert_amd_load_opts.restype = ctypes.c_void_p
+    L.bert_amd_load_opts.argtypes = [ctypes.c_char_p, I_P, ctypes.c_int32, ctypes.c_char_p]
     L.bert_amd_n_devices.restype = ctypes.c_int32
     L.bert_amd_n_devices.argtypes = [ctypes.c_void_p]
     L.bert_amd_hparams.restype = ctypes.c_int32
@@ -95,6 +98,8 @@ def lib() -> ctypes.CDLL:
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.bert_amd_debug_embed.restype = ctypes.c_int32
     L.bert_amd_debug_embed.argtypes = [ctypes.c_void_p, I_P, I_P, ctypes.c_int32, F_P, ctypes.c_void_p, ctypes.c_void_p]
+    L.bert_amd_debug_layers.restype = ctypes.c_int32
+    L.bert_amd_debug_layers.argtypes = [ctypes.c_void_p, I_P, I_P, ctypes.c_int32, F_P, ctypes.c_void_p, ctypes.c_void_p]
     L.bert_amd_set_option.restype = ctypes.c_int32
     L.bert_amd_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
     L.bert_amd_workspace_rows.restype = ctypes.c_int64
@@ -138,14 +143,19 @@ def quantize(src: str, dst: str, ftype: str) -> bool:
 class BertModel:
     """Mirror of examples/sample_dylib.py's BertModel, on the GPU library."""
 
-    def __init__(self, fname: str, devices: Sequence[int] | None = None):
+    def __init__(self, fname: str, devices: Sequence[int] | None = None, options: str | dict | None = None):
+        """devices: replica devices (None: bert_load_from_file, every visible one);
+        options: bert_amd_load_opts' "key=value;..." string or a dict of them."""
         L = lib()
         self.lib = L
-        if devices is None:
+        if isinstance(options, dict):
+            options = ";".join(f"{k}={v}" for k, v in options.items())
+        if devices is None and options is None:
             self.ctx = L.bert_load_from_file(fname.encode("utf-8"))
         else:
-            arr = (ctypes.c_int32 * len(devices))(*devices)
-            self.ctx = L.bert_amd_load(fname.encode("utf-8"), arr, len(devices))
+            arr = (ctypes.c_int32 * len(devices))(*devices) if devices else None
+            self.ctx = L.bert_amd_load_opts(fname.encode("utf-8"), arr, len(devices) if devices else 0,
+                                            options.encode() if options else None)
         if not self.ctx:
             raise RuntimeError(f"failed to load {fname}: {last_error()}")
         self.n_embd = L.bert_n_embd(self.ctx)
@@ -256,8 +266,26 @@ class BertModel:
             raise RuntimeError(f"bert_amd_debug_embed failed ({rc}): {last_error()}")
         return X, q, d
 
+    def debug_layers(self, token_lists):
+        """The residual stream after every stage (bert_amd_debug_layers): X f32
+        [n_layer + 1, M, E], q [n_layer + 1, M, E] and d [n_layer + 1, M, E/32]
+        (None for F16 / F32) — stage 0 the embeddings + LN, stage l + 1 layer l."""
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(t, np.int32) for t in token_lists]))
+        offs = np.zeros(len(token_lists) + 1, np.int32)
+        offs[1:] = np.cumsum([len(t) for t in token_lists])
+        M, E, wt, S = len(ids), self.n_embd, self.hparams[6], self.hparams[5] + 1
+        X = np.zeros((S, M, E), np.float32)
+        q = np.zeros((S, M, E), {0: np.float32, 1: np.float16, 2: np.int8, 3: np.int8}[wt])
+        d = np.zeros((S, M, E // 32), np.float16 if wt == 2 else np.float32) if wt in (2, 3) else None
+        rc = self.lib.bert_amd_debug_layers(self.ctx, ids.ctypes.data_as(I_P), offs.ctypes.data_as(I_P),
+                                            len(token_lists), X.ctypes.data_as(F_P), q.ctypes.data_as(ctypes.c_void_p),
+                                            d.ctypes.data_as(ctypes.c_void_p) if d is not None else None)
+        if rc != 0:
+            raise RuntimeError(f"bert_amd_debug_layers failed ({rc}): {last_error()}")
+        return X, q, d
+
     def set_option(self, key: str, value: int) -> None:
-        """bert_amd_set_option: "split" (0/1), "pack" (-1/0/1); results are identical either way."""
+        """bert_amd_set_option (include/bert_amd.h); results are identical under every setting."""
         if self.lib.bert_amd_set_option(self.ctx, key.encode(), int(value)) != 0:
             raise ValueError(f"bert_amd_set_option({key}, {value}) failed: {last_error()}")
 

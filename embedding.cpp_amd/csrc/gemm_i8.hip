@@ -43,19 +43,6 @@ typedef int int16v __attribute__((ext_vector_type(16)));
 #ifndef I8_UP_T
 #define I8_UP_T 2
 #endif
-// FFN-up output tile staged through LDS for coalesced stores (A/B: measured
-// 284 vs 279-281 µs unstaged on the headline batch, so off; -DI8_UP_STAGE=1)
-#ifndef I8_UP_STAGE
-#define I8_UP_STAGE 0
-#endif
-
-// development ablations (tools/f6_abl_libs.sh builds variants; timing only,
-// results wrong): bit 0 = no weight loads in the main loop; fused FFN: bit 1 =
-// no weight loads, bit 2 = no GELU / U stores, bit 3 = no residual loads, bit 4 =
-// no LN epilogue stores
-#ifndef I8_ABL
-#define I8_ABL 0
-#endif
 
 constexpr int I8_KC = 128;          // K per LDS chunk: 4 quant blocks (one scale vector)
 constexpr int I8_LDQ = I8_KC + 16;  // token row stride of the LDS chunk, bytes: ds_read_b128 conflict-free
@@ -189,9 +176,6 @@ struct I8Pipe {
     // block b - nkb of the next tile at ft0n) into ring slot S
     template <int S>
     __device__ __forceinline__ void wload(const GemmArgs &g, int nkb, int ft0, int ft0n, int b) {
-#if I8_ABL & 1
-        if (b >= 2) return;  // ablation (timing only, results wrong): no weight streaming after the prime
-#endif
         const bool nx = b >= nkb;
         const int ft = nx ? ft0n : ft0, bb = nx ? b - nkb : b;
 #pragma unroll
@@ -380,35 +364,6 @@ __device__ __forceinline__ void i8_store_q8_half(const ActPtr &out, int64_t ld, 
     }
 }
 
-// The same quantiser into a row-major LDS stage of an output tile: q bytes at
-// qst[r * ldq + 32 blk + 16 hh ..], the block scale at dst[r * nblk + blk]
-// (fp16 for Q8_0, f32 for Q8_1).
-template <int WT>
-__device__ __forceinline__ void i8_q8_half_stage(char *qst, int ldq, void *dst, int nblk, int r, int blk, int hh,
-                                                 const float (&y)[16]) {
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; i++) amax = fmaxf(amax, fabsf(y[i]));
-    {
-        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
-        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
-    }
-    float d, id;
-    q8_scales(amax, d, id);
-    uint4 pk;
-    pk.x = q8_pack4(y[0], y[1], y[2], y[3], id);
-    pk.y = q8_pack4(y[4], y[5], y[6], y[7], id);
-    pk.z = q8_pack4(y[8], y[9], y[10], y[11], id);
-    pk.w = q8_pack4(y[12], y[13], y[14], y[15], id);
-    *(uint4 *)(qst + r * ldq + 32 * blk + 16 * hh) = pk;
-    if (hh == 0) {
-        if constexpr (WT == W_Q4_0)
-            ((uint16_t *)dst)[r * nblk + blk] = f2h(d);
-        else
-            ((float *)dst)[r * nblk + blk] = d;
-    }
-}
-
 // XCD-aware tile order (as gemm_kernel): linear ids are dealt round-robin over
 // the 8 XCDs; each XCD walks a contiguous range, n fastest.
 __device__ __forceinline__ int xcd_linear(int orig, int nwg) {
@@ -429,14 +384,6 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
     using C = I8Chunk<BM, WT == W_Q4_1>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ __attribute__((aligned(16))) uint16_t gtab[GELU_FLAT_LDS];
-#if I8_UP_STAGE
-    // the output tile (Q8 bytes and block scales) staged for coalesced stores:
-    // whole 16-byte pieces of consecutive columns by consecutive threads instead
-    // of each lane's 16 bytes of its own row
-    constexpr int LDU = BN + (WT == W_Q4_1 ? 0 : 16), NBLK = BN / 32, DS = WT == W_Q4_1 ? 4 : 2;
-    __shared__ __attribute__((aligned(16))) char ust[BM * LDU];
-    __shared__ __attribute__((aligned(16))) char dst_[BM * NBLK * DS];
-#endif
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int nflat8 = (0x8000 + g.gelu.neg_n + 1 + 7) / 8;
     for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)g.gelu.full)[i];
@@ -480,31 +427,9 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
                 float y[16];
 #pragma unroll
                 for (int i = 0; i < 16; i++) y[i] = h2f(gtab[f2h(fmaxf(bias[i] + acc[f][t][i], xlo))]);
-#if I8_UP_STAGE
-                i8_q8_half_stage<WT>(ust, LDU, dst_, NBLK, 32 * (tw + t) + l32, fw + f, hh, y);
-#else
                 i8_store_q8_half<WT>(g.out_act, g.N, mc + 32 * (tw + t) + l32, fc + f, hh, y);
-#endif
             }
         }
-#if I8_UP_STAGE
-        __syncthreads();
-        {
-            // q: BM rows x BN bytes; d: BM rows x NBLK scales (row-contiguous in U)
-            const int64_t col0 = 32 * (int64_t)(fc - fw);
-#pragma unroll
-            for (int k = 0; k < BM * BN / 16 / NT; k++) {
-                const int i = tid + NT * k, r = i / (BN / 16), c = i - r * (BN / 16);
-                *(uint4 *)((int8_t *)g.out_act.q + (mc + r) * g.N + col0 + 16 * c) = *(const uint4 *)(ust + r * LDU + 16 * c);
-            }
-            constexpr int DPR = NBLK * DS / 16;  // 16-byte pieces of scales per row
-            if (tid < BM * DPR) {
-                const int r = tid / DPR, c = tid - r * DPR;
-                *(uint4 *)((char *)g.out_act.d + ((mc + r) * (g.N / 32) + (fc - fw)) * DS + 16 * c) =
-                    *(const uint4 *)(dst_ + (r * NBLK) * DS + 16 * c);
-            }
-        }
-#endif
     }
 }
 
@@ -634,315 +559,6 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
 }
 
 // ---------------------------------------------------------------------------
-// Fused FFN for n_embd = 384 (bert.cpp:965-992): X = LN(X + b2 + W2 . q8(gelu(b1 +
-// W1 . x))) in one kernel, so the intermediate U (1536 features per row) never
-// leaves the workgroup.  One 12-wave workgroup per CU walks 64-row tiles
-// (persistent).  The tile's Q8 input x (64 x 384) stays resident in LDS; the
-// intermediate is produced and consumed in 384-feature slices j = 0 .. I/384 - 1:
-//   up_j:   acc_u = x . W1[slice j]^T          (wave w: features 384 j + 32 w ..)
-//           U_j   = q8(gelu(b1 + acc_u))       ggml's fp16 GELU table, Q8 blocks of 32,
-//                                              into LDS in the int8 main loop's chunk layout
-//   down_j: acc_d += U_j . W2[:, slice j]^T    (wave w: output features 32 w ..)
-// ggml quantises the whole U row block by block (quantize_row_q8_x) and sums the
-// K blocks of the down projection in order; the slices keep both (blocks are
-// independent, and acc_d runs over the blocks in the same order).  Then the
-// LayerNorm epilogue of i8_ln384_kernel with the residual read per lane.
-// Weights stream from L2 through a 4-slot register ring along the fixed
-// per-tile block sequence (up_0, down_0, up_1, ..., down_last: 24 I/384
-// blocks), which repeats for the next tile, so the ring runs across phases and
-// tiles; the next tile's x is loaded during the last down phase.
-template <int WT>
-struct FfnPipe {
-    static constexpr bool Q1 = WT == W_Q4_1;
-    int4v wf[4][1];
-    uint2 wr[1];             // Q4_0: fp16 d_w of the next chunk's 4 blocks
-    float4v wdr[1], wmr[1];  // Q4_1
-    I8Items<1> st;           // this thread's (row, block) item of the next tile's x
-    int nj, qt, ct;          // slices, blocks and 4-block chunks per tile
-    int wv;                  // wave index (uniform)
-
-    // weight fragments of block q of the per-tile sequence (mod qt) into slot S;
-    // u.Wi is the wave-major stream of runtime.cpp upload_ffn_i8
-    template <int S>
-    __device__ __forceinline__ void wload(const GemmArgs &u, int q) {
-        q = q >= qt ? q - qt : q;
-#if I8_ABL & 2
-        if (q >= 2) return;
-#endif
-        wf[S][0] = ((const int4v *)u.Wi.q)[(int64_t)(wv * qt + q) * 64 + (threadIdx.x & 63)];
-    }
-    // scale vectors of 4-block chunk c of the sequence (mod ct)
-    __device__ __forceinline__ void sload(const GemmArgs &u, int c) {
-        c = c >= ct ? c - ct : c;
-        const int64_t at = (int64_t)(wv * ct + c) * 32 + (threadIdx.x & 31);
-        if constexpr (Q1) {
-            wdr[0] = ((const float4v *)u.Wi.d)[at];
-            wmr[0] = ((const float4v *)u.Wi.m)[at];
-        } else {
-            wr[0] = ((const uint2 *)u.Wi.dh)[at];
-        }
-    }
-    // this thread's item into the resident x (I8Chunk layout, as i8_stage_store)
-    __device__ __forceinline__ void xstore(char *xbuf) const {
-        using C = I8Chunk<64, Q1>;
-        const int t = threadIdx.x, c = t >> 8, it = t & 255, r = it >> 2, bb = it & 3;
-        char *buf = xbuf + c * C::BYTES;
-        int4v *q = (int4v *)(buf + r * I8_LDQ + 32 * bb);
-        q[0] = st.q0[0];
-        q[1] = st.q1[0];
-        if constexpr (Q1) {
-            ((float *)(buf + C::QB))[bb * 64 + r] = st.d[0];
-            int sq = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) sq = __builtin_amdgcn_sdot4(st.q0[0][j], 0x01010101, sq, false);
-#pragma unroll
-            for (int j = 0; j < 4; j++) sq = __builtin_amdgcn_sdot4(st.q1[0][j], 0x01010101, sq, false);
-            ((float *)(buf + C::QB + C::DB))[bb * 64 + r] = st.d[0] * (float)sq;
-        } else {
-            ((uint16_t *)(buf + C::QB))[bb * 64 + r] = st.d16[0];
-        }
-    }
-    // this thread's item of x (tile at m0): chunk tid / 256, (row, block) of it
-    __device__ __forceinline__ void xload(const GemmArgs &u, int64_t m0) {
-        const int t = threadIdx.x, c = t >> 8, it = t & 255, r = it >> 2, bb = it & 3;
-        const int64_t row = m0 + r;
-        const int4v *p = (const int4v *)((const int8_t *)u.A.q + row * 384 + 128 * c + 32 * bb);
-        st.q0[0] = p[0];
-        st.q1[0] = p[1];
-        const int64_t bi = row * 12 + 4 * c + bb;
-        if constexpr (Q1)
-            st.d[0] = ((const float *)u.A.d)[bi];
-        else
-            st.d16[0] = ((const uint16_t *)u.A.d)[bi];
-    }
-};
-
-// Q8 block of 32 consecutive values held as 16 per lane by lanes l and l ^ 32
-// into an LDS chunk (I8Chunk layout, block bb of the chunk, token row r)
-template <int WT, int BM>
-__device__ __forceinline__ void i8_q8_half_lds(char *buf, int r, int bb, int hh, const float (&y)[16]) {
-    using C = I8Chunk<BM, WT == W_Q4_1>;
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; i++) amax = fmaxf(amax, fabsf(y[i]));
-    {
-        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
-        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
-    }
-    float d, id;
-    q8_scales(amax, d, id);
-    int4v pk;
-    pk[0] = (int)q8_pack4(y[0], y[1], y[2], y[3], id);
-    pk[1] = (int)q8_pack4(y[4], y[5], y[6], y[7], id);
-    pk[2] = (int)q8_pack4(y[8], y[9], y[10], y[11], id);
-    pk[3] = (int)q8_pack4(y[12], y[13], y[14], y[15], id);
-    *(int4v *)(buf + r * I8_LDQ + 32 * bb + 16 * hh) = pk;
-    if constexpr (WT == W_Q4_1) {
-        // ggml quantize_row_q8_1: s = d * (float) sum_j q_j over the block
-        int sq = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) sq = __builtin_amdgcn_sdot4(pk[j], 0x01010101, sq, false);
-        const auto o = __builtin_amdgcn_permlane32_swap((uint32_t)sq, (uint32_t)sq, false, false);
-        sq = (int)o[0] + (int)o[1];
-        if (hh == 0) {
-            ((float *)(buf + C::QB))[bb * BM + r] = d;
-            ((float *)(buf + C::QB + C::DB))[bb * BM + r] = d * (float)sq;
-        }
-    } else {
-        if (hh == 0) ((uint16_t *)(buf + C::QB))[bb * BM + r] = f2h(d);
-    }
-}
-
-template <int WT>
-__global__ __launch_bounds__(768) void i8_ffn384_kernel(GemmArgs u, GemmArgs d, int n_mtiles) {
-    constexpr int NT = 768, BM = 64, F = 1, T = 2, NCOL = 384, NWV = 12;
-    constexpr bool Q1 = WT == W_Q4_1;
-    using C = I8Chunk<BM, Q1>;
-    __shared__ __attribute__((aligned(16))) char xbuf[3 * C::BYTES];  // the tile's x: 3 chunks of 4 blocks
-    __shared__ __attribute__((aligned(16))) char ubuf[3 * C::BYTES];  // U slice j: 3 chunks of 4 blocks
-    __shared__ __attribute__((aligned(16))) uint32_t gtab[HALF_TABLE_LDS / 2];  // GELU pair view
-    __shared__ double red[2][NWV][BM];
-    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if ((int)blockIdx.x >= n_mtiles) return;
-    for (int i = tid; i < u.gelu.n_pad / 8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)u.gelu.compact)[i];
-    const uint32_t cap = (uint32_t)u.gelu.cap;
-    const float4v z4 = {0.f, 0.f, 0.f, 0.f};
-
-    FfnPipe<WT> pp;
-    pp.nj = d.K / NCOL;
-    pp.qt = 24 * pp.nj;
-    pp.ct = 6 * pp.nj;
-    pp.wv = wv;
-    int64_t m0n = (int64_t)xcd_linear(blockIdx.x, n_mtiles) * BM;
-    pp.xload(u, m0n);
-    pp.template wload<0>(u, 0);
-    pp.template wload<1>(u, 1);
-    pp.sload(u, 0);
-    pp.xstore(xbuf);
-    int4v ws[F];
-    float4v wd[F], wm[F];
-    auto wscale_use = [&]() {
-        if constexpr (Q1) {
-            wd[0] = hh ? z4 : pp.wdr[0];
-            wm[0] = pp.wmr[0];
-        } else {
-            ws[0] = int4v{(int)pp.wr[0].x, (int)pp.wr[0].y, (int)pp.wr[0].x, (int)pp.wr[0].y};
-        }
-    };
-    wscale_use();
-    __syncthreads();
-
-    // one 4-block chunk of a phase at LDS `buf` (q: the sequence index of its
-    // first block, c: the chunk's sequence index), accumulating into acc
-    auto chunk = [&](const char *buf, int q, int c, float16v (&acc)[F][T]) {
-        I8AOps<T> a0, a1;
-        i8_aops<WT, BM, T, 0>(a0, buf, 0);
-        i8_block<WT, BM, F, T, 0, true>(buf, 0, pp.wf[0], ws, wd, wm, a0, a1, acc);
-        pp.template wload<2>(u, q + 2);
-        i8_block<WT, BM, F, T, 1, true>(buf, 0, pp.wf[1], ws, wd, wm, a1, a0, acc);
-        pp.template wload<3>(u, q + 3);
-        pp.sload(u, c + 1);
-        i8_block<WT, BM, F, T, 2, true>(buf, 0, pp.wf[2], ws, wd, wm, a0, a1, acc);
-        pp.template wload<0>(u, q + 4);
-        i8_block<WT, BM, F, T, 3, true>(buf, 0, pp.wf[3], ws, wd, wm, a1, a0, acc);
-        pp.template wload<1>(u, q + 5);
-        wscale_use();
-    };
-
-    for (int tile = blockIdx.x; tile < n_mtiles; tile += gridDim.x) {
-        const int64_t m0 = m0n;
-        const bool has_next = tile + (int)gridDim.x < n_mtiles;
-        if (has_next) m0n = (int64_t)xcd_linear(tile + gridDim.x, n_mtiles) * BM;
-        float16v acc_d[F][T];
-#pragma unroll
-        for (int t = 0; t < T; t++) acc_d[0][t] = float16v{};
-        // up_j and U slice j into LDS
-        auto up_phase = [&](int j) {
-            float16v acc_u[F][T];
-#pragma unroll
-            for (int t = 0; t < T; t++) acc_u[0][t] = float16v{};
-#pragma unroll 1
-            for (int c = 0; c < 3; c++) chunk(xbuf + c * C::BYTES, 24 * j + 4 * c, 6 * j + c, acc_u);
-            __syncthreads();  // the previous down phase has finished reading ubuf
-            const int col = NCOL * j + 32 * wv + 16 * hh;
-            float bias[16];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float4v b4 = *(const float4v *)(u.bias + col + 4 * q);
-#pragma unroll
-                for (int k = 0; k < 4; k++) bias[4 * q + k] = b4[k];
-            }
-#if !(I8_ABL & 4)
-#pragma unroll
-            for (int t = 0; t < T; t++) {
-                float y[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) y[i] = h2f((uint16_t)gelu_lookup(gtab, cap, f2h(bias[i] + acc_u[0][t][i])));
-                i8_q8_half_lds<WT, BM>(ubuf + (wv >> 2) * C::BYTES, 32 * t + l32, wv & 3, hh, y);
-            }
-#else
-            if (bias[0] + acc_u[0][0][0] + acc_u[0][1][5] == 12345.f) ubuf[tid] = 1;
-#endif
-            __syncthreads();
-        };
-        auto down_phase = [&](int j) {
-#pragma unroll 1
-            for (int c = 0; c < 3; c++) chunk(ubuf + c * C::BYTES, 24 * j + 12 + 4 * c, 6 * j + 3 + c, acc_d);
-        };
-        const int nj = pp.nj;
-#pragma unroll 1
-        for (int j = 0; j < nj - 1; j++) {
-            up_phase(j);
-            down_phase(j);
-        }
-        up_phase(nj - 1);
-        // the residual rows of this lane, and the next tile's x (its LDS slot is
-        // free: the last up phase is behind up_phase's barriers)
-        float4v xr[T][4];
-#pragma unroll
-        for (int t = 0; t < T; t++) {
-            const float4v *xp = (const float4v *)(d.X + (m0 + 32 * t + l32) * NCOL + 32 * wv + 16 * hh);
-#pragma unroll
-            for (int q = 0; q < 4; q++) xr[t][q] = (I8_ABL & 8) ? z4 : xp[q];
-        }
-        if (has_next) pp.xload(u, m0n);
-        down_phase(nj - 1);
-        if (has_next) pp.xstore(xbuf);
-        // LayerNorm epilogue (i8_ln384_kernel's, residual from registers);
-        // its barriers also publish the next tile's x
-        const int col = 32 * wv + 16 * hh;
-#pragma unroll
-        for (int t = 0; t < T; t++) {
-            const int r = 32 * t + l32;
-            double s = 0.0;
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                const float4v b4 = *(const float4v *)(d.bias + col + 4 * qq);
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const float v = (b4[k] + acc_d[0][t][4 * qq + k]) + xr[t][qq][k];
-                    acc_d[0][t][4 * qq + k] = v;
-                    s += (double)v;
-                }
-            }
-            s += __shfl_xor(s, 32);
-            if (hh == 0) red[0][wv][r] = s;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < T; t++) {
-            const int r = 32 * t + l32;
-            double tot = 0.0;
-#pragma unroll
-            for (int w = 0; w < NWV; w++) tot += red[0][w][r];
-            const float mean = (float)(tot / NCOL);
-            double s2 = 0.0;
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const float v = acc_d[0][t][i] - mean;
-                acc_d[0][t][i] = v;
-                s2 += (double)(v * v);
-            }
-            s2 += __shfl_xor(s2, 32);
-            if (hh == 0) red[1][wv][r] = s2;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < T; t++) {
-            const int r = 32 * t + l32;
-            const int64_t row = m0 + r;
-            double tot = 0.0;
-#pragma unroll
-            for (int w = 0; w < NWV; w++) tot += red[1][w][r];
-            const float var = (float)(tot / NCOL);
-            const float scale = 1.0f / sqrtf(var + d.eps);
-            float y[16];
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                const float4v w4 = *(const float4v *)(d.ln_w + col + 4 * qq);
-                const float4v b4 = *(const float4v *)(d.ln_b + col + 4 * qq);
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    float z = acc_d[0][t][4 * qq + k] * scale;
-                    z = w4[k] * z;
-                    y[4 * qq + k] = z + b4[k];
-                }
-#if !(I8_ABL & 16)
-                *(float4v *)(d.X + row * NCOL + col + 4 * qq) = float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
-#endif
-            }
-#if !(I8_ABL & 16)
-            i8_store_q8_half<WT>(d.out_act, NCOL, row, wv, hh, y);
-#else
-            if (y[0] + y[7] == 12345.f) d.X[row] = 1.f;
-#endif
-        }
-        // `red` is rewritten only after the next tile's first phases' barriers
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Projection + residual for rows too wide for one workgroup (n_embd 768 /
 // 1024): X = (b + W.x) + X; LayerNorm then runs in launch_ln.
 template <int WT>
@@ -1029,21 +645,6 @@ static hipError_t i8_gemm_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s)
         hipLaunchKernelGGL((i8_resid_kernel<WT>), dim3(persistent_grid(mt * nt)), dim3(512), 0, s, a, mt, nt);
     } else {
         return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-bool i8_ffn_supported(int E, int I) { return E == 384 && I % 384 == 0 && I > 0; }
-
-hipError_t launch_ffn_i8(int wtype, const GemmArgs &u, const GemmArgs &d, int Mpad, hipStream_t s) {
-    if (!i8_ffn_supported(u.K, d.K) || u.N != d.K || d.N != u.K || Mpad % 64 || u.gelu.n_pad > HALF_TABLE_LDS ||
-        (int64_t)u.gelu.cap * 2 + 2 > u.gelu.n_pad)
-        return hipErrorInvalidValue;
-    const int mt = Mpad / 64;
-    switch (wtype) {
-        case W_Q4_0: hipLaunchKernelGGL((i8_ffn384_kernel<W_Q4_0>), dim3(persistent_grid(mt)), dim3(768), 0, s, u, d, mt); break;
-        case W_Q4_1: hipLaunchKernelGGL((i8_ffn384_kernel<W_Q4_1>), dim3(persistent_grid(mt)), dim3(768), 0, s, u, d, mt); break;
-        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

@@ -25,18 +25,10 @@ namespace bertamd {
 // follows it exactly like ggml's vec_dot_type:
 //   W_F32 -> f32, W_F16 -> fp16 (RNE), W_Q4_0 -> Q8_0 (int8 + fp16 d),
 //   W_Q4_1 -> Q8_1 (int8 + f32 d)
-// W_Q4_0D: Q4_0 weights whose GEMMs run on the block-scaled fp6 MFMA
-// (gemm_f6.hip); the same ggml Q8_0 activations (d, q), stored as Q8D: per
-// 32-block 48 bytes of fp6 digit codes (kernels_common.h q8d_*) + fp16 d.
-enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3, W_Q4_0D = 4, W_Q4_0N = 5, W_Q4_1N = 6 };
-// W_Q4_0N / W_Q4_1N: Q4 weights kept as ggml's nibbles and dequantised inside
-// the fp16 MFMA GEMM (WPtr below); their activations are Q4_0's / Q4_1's
-// (ggml Q8_0 / Q8_1).
-constexpr int act_of(int wt) { return wt == W_Q4_0N ? W_Q4_0 : wt == W_Q4_1N ? W_Q4_1 : wt; }
-constexpr int Q8D_BLK = 48;  // code bytes per Q8D block
+enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3 };
 
 struct ActPtr {
-    void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K] | Q8D codes [M][K/32][48 B]
+    void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K]
     void *d = nullptr;  // per-32-block scale [M][K/32]: fp16 (Q8_0) | f32 (Q8_1)
 };
 
@@ -51,22 +43,11 @@ struct ActPtr {
 //         lo = fp16(w - hi).  For Q4_0 the split is exact (w has <= 15
 //         significant bits), so an fp16 MFMA over integer Q8 activations
 //         returns d_w * sum(q_a * q_w) exactly in each product; `unscale` = 2^-S.
-//   Q4_0N: q = uint32 [N/16][K/32][64]: lane (c, g)'s 8 nibbles q (k = 8 g + j
-//         at bits 4 (j >> 1) + 16 (j & 1), so one and-or per pair makes two
-//         fp16 integers 1024 + q); d = fp16 [N/16][K/32][16] (d_w of column c).
-//         The MFMA takes q - 8 as exact fp16 integers against the Q8 codes
-//         (isum exact in f32) and the fold applies d_w * d_a per block, as
-//         ggml_vec_dot_q4_0_q8_0; 0.56 B per weight.
-//   Q4_1N: q = uint32 [N/16][K/32][64][2] (plain main loop only): the 8
-//         nibbles q (same bit order as Q4_0N) and the fp16 d | m << 16 of
-//         column c; the fold adds ggml's m_w * s_a term per block
-//         (vec_dot_q4_1_q8_1: d_w d_a isum + m_w s_a, s_a = d_a sum(q_a)).
 //   F16 : q = fp16 [N/16][K/32][64][8]
 //   F32 : q = f32  [N/16][K/32][64][8]
 struct WPtr {
     const void *q = nullptr;
     float unscale = 1.f;
-    const uint16_t *d = nullptr;  // Q4_0N block scales
 };
 
 // Q4_0 / Q4_1 weights for the int8-MFMA GEMMs (gemm_i8.hip), repacked at load
@@ -85,28 +66,12 @@ struct I8W {
     const uint16_t *dh = nullptr;
 };
 
-// Q4_0 weights for the fp6-MFMA GEMMs (gemm_f6.hip), repacked at load
-// (runtime.cpp upload_f6) per 32-row f-tile ft (features 32 ft .. 32 ft + 31,
-// natural order) and 32-wide k block b: the 32 codes of q - 8 (e2m3
-// sign-magnitude, 6 bits each, element k at Q8D position q8d_pos(k)) as
-//   q16: [N/32][K/32][32 rows] x 16 B (code dwords 0-3)
-//   q8 : [N/32][K/32][32 rows] x 8 B  (code dwords 4-5)
-//   dw : [N/32][K/128][32 rows] x 4 dwords: dword v = fp16 d_w of block 4 g + v
-//        in the low half (the d_w operand of the d_w * d_a MFMA)
-struct F6W {
-    const uint4 *q16 = nullptr;
-    const uint2 *q8 = nullptr;
-    const uint4 *dw = nullptr;
-};
-
 enum Epi : int {
     EPI_QKV = 0,       // y = b + W.x split hi/lo for attention (Q|K row-major, V transposed)
     EPI_GELU_ACT = 1,  // gelu(b + W.x) in the next matmul's activation format
     EPI_LN = 2,        // LN((b + W.x) + X) -> X and activation format (the workgroup owns whole rows)
     EPI_RESID = 3,     // (b + W.x) + X -> X; LayerNorm then runs in launch_ln (rows too wide for one tile)
-    EPI_NONE = 4,      // main-loop probe (tools/gemm_bench): nothing stored
-    EPI_RESLN = 5      // EPI_RESID over all of a row tile's column tiles in one workgroup, then
-                       // LayerNorm of its rows -> X and activation format (Q4 weights, N 768 / 1024)
+    EPI_NONE = 4       // main-loop probe (tools/gemm_bench): nothing stored
 };
 
 // Piecewise view of a 65536-entry fp16 -> fp16 table (ggml's GELU / exp
@@ -133,7 +98,6 @@ struct GemmArgs {
     int K = 0;
     WPtr W;                // [N][K] repacked
     I8W Wi;                // the same weights for the int8 path (Q4 GEMMs in gemm_i8.hip)
-    F6W Wf;                // the same weights for the fp6 path (Q4_0 GEMMs in gemm_f6.hip)
     int N = 0;
     const float *bias = nullptr;   // [N]
     // EPI_QKV: y = b + W.x (f32, as ggml), stored split for the attention MFMAs:
@@ -188,14 +152,14 @@ hipError_t launch_gemm(int wtype, int epi, int E_or_bn, const GemmArgs &a, int M
 hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs, int max_len, hipStream_t s);
 // whether packing n_seqs sentences into n_tiles workgroups is worth the packed variant
 bool qkv_attention_pack_pays(int n_seqs, int n_tiles);
-// QKV GEMM + attention in one kernel (sentences <= 128 tokens, head dim 32);
-// g: the QKV GemmArgs (head-major weights), a: the AttnArgs (its Q/K/V pointers unused)
-bool qkv_attention_supported(int wtype, int E, int H, int max_len);
-// head pairs per GEMM main loop of that kernel (its QKV copy's tile grouping, runtime.cpp)
-int qkv_attention_ntw(int wtype);
-// n_blocks: tiles (a.tiles) or sentences (a.tiles == null); wtype W_Q4_0D: Q4_0
-// weights, int8 Q8_0 input, context stored as Q8D
-hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s);
+// QKV GEMM + attention in one kernel (sentences <= 128 tokens, head dim 32 or
+// 64); g: the QKV GemmArgs (head-major weights in the kernel's grouped tile
+// order), a: the AttnArgs (its Q/K/V pointers unused).  ntw: 192-feature
+// units (head pairs at head dim 32) per GEMM main loop, 1 or 2 — the grouping
+// of the kernel's QKV weight copy (runtime.cpp), chosen per context at load.
+bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw);
+// n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s);
 // out_row (optional): output row of each sentence (default: its batch index)
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s,
                        const int32_t *out_row = nullptr);
@@ -215,20 +179,5 @@ bool gemm_gelu_blk8(int wtype);
 // EPI_LN (N == 384), EPI_RESID (N % 256 == 0); K % 128 == 0; Mpad % 128 == 0.
 bool i8_gemm_supported(int epi, int N, int K);
 hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
-// The whole FFN of an n_embd 384 layer in one kernel (gemm_i8.hip
-// i8_ffn384_kernel): u = the FFN-up GemmArgs (A = Xa, bias, gelu pair view, and
-// in Wi the weight stream of both projections, runtime.cpp upload_ffn_i8),
-// d = the FFN-down + LN GemmArgs (Wi, bias, X, ln_w / ln_b, eps, out_act);
-// u.A and d.out_act may be the same buffer.  I % 384 == 0; Mpad % 64 == 0.
-bool i8_ffn_supported(int E, int I);
-hipError_t launch_ffn_i8(int wtype, const GemmArgs &u, const GemmArgs &d, int Mpad, hipStream_t s);
-
-// Q4_0 x Q8D GEMMs on the fp6 MFMA (gemm_f6.hip): A in Q8D; EPI_GELU_ACT
-// (N % 512 == 0, output Q8D), EPI_LN (N == 384, output `out_type` W_Q4_0D or
-// ggml's Q8_0 W_Q4_0); K 384 or 1536; Mpad % 128 == 0.
-bool f6_gemm_supported(int epi, int N, int K);
-hipError_t launch_gemm_f6(int epi, const GemmArgs &a, int Mpad, hipStream_t s, int out_type = W_Q4_0D);
-// Q8_0 (int8 q [nblk][32]) <-> Q8D codes [nblk][48 B]; the fp16 d are shared
-hipError_t launch_q8_convert(bool to_q8d, const void *src, void *dst, int64_t nblk, hipStream_t s);
 
 }  // namespace bertamd

@@ -282,8 +282,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
 // slices).  Statistics as ggml_norm: mean = double sum / E, then the double
 // sum of the f32 squares of (x - mean).  A row's 32-wide block partials are
 // summed in block order by one thread per row (not by every lane of the row),
-// which then writes the row's mean / scale.  Shared by ln_rows_kernel and the
-// GEMM's EPI_RESLN epilogue, so both give the same bits.
+// which then writes the row's mean / scale.
 template <int WT, int NBLK, int NT>
 __device__ __forceinline__ void ln_rows16(float *X, const float *__restrict__ lnw, const float *__restrict__ lnb,
                                           float eps, const ActPtr &out, int64_t row0, double *red, float *stat) {
@@ -437,9 +436,7 @@ __device__ __forceinline__ void i8x4_to_f16(uint32_t x, half2v &lo, half2v &hi) 
     hi = __builtin_bit_cast(half2v, h) - off;
 }
 
-// SA (Q4_1N GEMMs): also s_a = d_a * sum(q_a) per (block, row), after the d_a
-// array (ggml's block_q8_1 s term); the block's two pieces are lanes l, l ^ 1.
-template <int WT, int BM, int LDA = LDA_H, int KBT = KB, bool SA = false>
+template <int WT, int BM, int LDA = LDA_H, int KBT = KB>
 __device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item, float unscale) {
     const int r = item / (2 * KBT), s = item % (2 * KBT);
     constexpr int A_BYTES = (WT == W_F32) ? BM * LDA_F * 4 : BM * LDA * 2;
@@ -458,15 +455,6 @@ __device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item,
         half8 *dst = (half8 *)((_Float16 *)buf + r * LDA + s * 16);
         dst[0] = h0;
         dst[1] = h1;
-        if constexpr (SA) {
-            int q = 0;
-            q = __builtin_amdgcn_sdot4((int)w.x, 0x01010101, q, false);
-            q = __builtin_amdgcn_sdot4((int)w.y, 0x01010101, q, false);
-            q = __builtin_amdgcn_sdot4((int)w.z, 0x01010101, q, false);
-            q = __builtin_amdgcn_sdot4((int)w.w, 0x01010101, q, false);
-            q += __shfl_xor(q, 1);
-            if ((s & 1) == 0) ((float *)(buf + A_BYTES))[KBT * BM + (s >> 1) * BM + r] = ar.d * (float)q;
-        }
         if ((s & 1) == 0) {
             float *sc = (float *)(buf + A_BYTES);  // [block of the chunk][BM]: d_a * 2^-S (exact)
             sc[(s >> 1) * BM + r] = ar.d * unscale;
@@ -486,11 +474,6 @@ __device__ __forceinline__ void a_store(const AReg<WT> &ar, char *buf, int item,
 
 template <int WT> struct WFrag;
 template <> struct WFrag<W_Q4_0> { half8 hi, lo; };
-// Q4_0N: one 16-byte record per lane: 8 nibbles, the fp16 d_w of columns
-// 4g .. 4g + 3 (transposed main loop) and of column c16 (plain)
-template <> struct WFrag<W_Q4_0N> { u32x4v r; };
-// Q4_1N: 8 nibbles and the column's fp16 d | m << 16
-template <> struct WFrag<W_Q4_1N> { u32x2v r; };
 template <> struct WFrag<W_Q4_1> { half8 hi, lo; };
 template <> struct WFrag<W_F16> { half8 h; };
 template <> struct WFrag<W_F32> { float4v f[2]; };
@@ -499,11 +482,7 @@ template <int WT>
 __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
     const int lane = threadIdx.x & 63;
     WFrag<WT> f;
-    if constexpr (WT == W_Q4_1N) {
-        f.r = ((const u32x2v *)W.q)[tile * 64 + lane];
-    } else if constexpr (WT == W_Q4_0N) {
-        f.r = ((const u32x4v *)W.q)[tile * 64 + lane];
-    } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         f.hi = ((const half8 *)W.q)[(tile * 2) * 64 + lane];
         f.lo = ((const half8 *)W.q)[(tile * 2 + 1) * 64 + lane];
     } else if constexpr (WT == W_F16) {
@@ -513,22 +492,6 @@ __device__ __forceinline__ WFrag<WT> w_load(const WPtr &W, int64_t tile) {
         f.f[1] = ((const float4v *)W.q)[(tile * 64 + lane) * 2 + 1];
     }
     return f;
-}
-
-// Q4_0N: 8 nibbles (k = 2 s + e at bits 4 s + 16 e) -> q - 8 as exact fp16
-// integers: (0x6400 | q) is 1024 + q, one and-or and one packed subtract per pair
-// (Q4_1N: q itself, OFF = 1024)
-template <int OFF = 1032>
-__device__ __forceinline__ half8 nib_to_f16(uint32_t x) {
-    const half2v off = {(_Float16)(float)OFF, (_Float16)(float)OFF};
-    half8 w;
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-        const half2v h = __builtin_bit_cast(half2v, ((x >> (4 * s)) & 0x000f000fu) | 0x64006400u) - off;
-        w[2 * s] = h[0];
-        w[2 * s + 1] = h[1];
-    }
-    return w;
 }
 
 // GEMM main loop, shared by gemm_kernel and qkv_attention_kernel:
@@ -541,23 +504,13 @@ __device__ __forceinline__ half8 nib_to_f16(uint32_t x) {
 // The loop's first loads (A chunk 0 into registers, W blocks 0 and 1) come
 // from a MainloopPre the caller filled with mainloop_preload, early enough
 // for their latency to hide behind other work where it can.
-// the Q4 fold on packed f32 ops (A/B: -DQP_FOLD_PK=0)
-#ifndef QP_FOLD_PK
-#define QP_FOLD_PK 1
-#endif
-
-// W blocks in flight in the main loop's register ring: 2 (split planes, F16),
-// QN_RING for nibble records (a quarter of the bytes, half the MFMAs per
-// block: the loads need more blocks of cover)
-#ifndef QN_RING
-#define QN_RING 4
-#endif
-constexpr int w_ring(int wt) { return wt == W_F32 ? 1 : (wt == W_Q4_0N || wt == W_Q4_1N) ? QN_RING : 2; }
+// W blocks in flight in the main loop's register ring: 2 (split planes, F16)
+constexpr int w_ring(int wt) { return wt == W_F32 ? 1 : 2; }
 
 template <int WT, int NW, int BM, int NTW, int KBT = KB>
 struct MainloopPre {
     static constexpr int IT = (BM * (2 * KBT) + NW * 64 - 1) / (NW * 64);
-    AReg<act_of(WT)> ar[IT];
+    AReg<WT> ar[IT];
     WFrag<WT> wf[w_ring(WT)][NTW];
 };
 
@@ -574,7 +527,7 @@ __device__ __forceinline__ void mainloop_preload(MainloopPre<WT, NW, BM, NTW, KB
         // scratch 64 -> 20 bytes per lane)
         int item = tid + it * NT;
         asm volatile("" : "+v"(item));
-        if (item < ITEMS) a_load<act_of(WT), KBT>(pre.ar[it], args.A, args.K, m0, 0, item);
+        if (item < ITEMS) a_load<WT, KBT>(pre.ar[it], args.A, args.K, m0, 0, item);
     }
     if constexpr (WT != W_F32) {
 #pragma unroll
@@ -594,12 +547,11 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     constexpr int KB = KBT, KC = 32 * KBT, LDA_H = KC + (KBT == 2 ? 16 : 8);
     constexpr int NT = NW * 64;
     constexpr int RT = BM / 16;
-    constexpr bool QN1 = WT == W_Q4_1N, QN = WT == W_Q4_0N || QN1, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
-    static_assert(!QN1 || !TRANS, "Q4_1N: plain main loop only");
-    constexpr int AT = act_of(WT);
+    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr int AT = WT;
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
-    constexpr int A_BUF = A_BYTES + (QP ? (QN1 ? 2 : 1) * KB * BM * 4 : 0);
+    constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
     const int tid = threadIdx.x, lane = tid & 63;
@@ -616,7 +568,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     for (int it = 0; it < IT; it++) {
         int item = tid + it * NT;
         asm volatile("" : "+v"(item));
-        if (item < ITEMS) a_store<AT, BM, LDA_H, KBT, QN1>(pre.ar[it], smem, item, unscale);
+        if (item < ITEMS) a_store<AT, BM, LDA_H, KBT>(pre.ar[it], smem, item, unscale);
     }
     // W fragments of the WR blocks in flight: block b lives in wf[b % WR] and
     // is replaced by block b + WR as soon as its MFMAs are issued; the chunk
@@ -658,10 +610,8 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                 const float *sc = (const float *)(abuf + A_BYTES) + kb * BM;
                 half8 a[RT];
                 float4v da[RT];  // TRANS: da[rt][0] = d_a of row 16 rt + c16
-                [[maybe_unused]] float4v sa[QN1 ? RT : 1];  // Q4_1N: s_a of the lane's rows
                 auto lds_a = [&](int rt) {
                     a[rt] = *(const half8 *)((const _Float16 *)abuf + (rt * 16 + c16) * LDA_H + kb * 32 + 8 * g);
-                    if constexpr (QN1) sa[rt] = *(const float4v *)(sc + KB * BM + rt * 16 + g * 4);
                     if constexpr (TRANS)
                         da[rt][0] = sc[rt * 16 + c16];
                     else
@@ -671,38 +621,9 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                     return TRANS ? __builtin_amdgcn_mfma_f32_16x16x32_f16(w, x, c, 0, 0, 0)
                                  : __builtin_amdgcn_mfma_f32_16x16x32_f16(x, w, c, 0, 0, 0);
                 };
-                // Q4_0N: the fragment's q - 8 as fp16 integers (one MFMA gives the
-                // block's isum exactly) and its d_w, per n-tile; the fold scales by
-                // d_a * d_w (exact in f32), as ggml_vec_dot_q4_0_q8_0
-                [[maybe_unused]] half8 wn[QN ? NTW : 1];
-                [[maybe_unused]] float4v dw[QN ? NTW : 1];
-                if constexpr (QN1) {  // Q4_1N: q as fp16 integers, d_w and m_w of the lane's column
-#pragma unroll
-                    for (int nt = 0; nt < NTW; nt++) {
-                        const u32x2v r = wf[SL][nt].r;
-                        wn[nt] = nib_to_f16<1024>(r.x);
-                        dw[nt][0] = h2f((uint16_t)r.y);
-                        dw[nt][1] = h2f((uint16_t)(r.y >> 16));
-                    }
-                } else if constexpr (QN) {
-#pragma unroll
-                    for (int nt = 0; nt < NTW; nt++) {
-                        const u32x4v r = wf[SL][nt].r;
-                        wn[nt] = nib_to_f16(r.x);
-                        if constexpr (TRANS)
-                            dw[nt] = float4v{h2f((uint16_t)r.y), h2f((uint16_t)(r.y >> 16)), h2f((uint16_t)r.z),
-                                             h2f((uint16_t)(r.z >> 16))};
-                        else
-                            dw[nt][0] = h2f((uint16_t)r.w);
-                    }
-                }
                 auto blk_of = [&](int rt_, int nt_) {
-                    if constexpr (QN) {
-                        return mfma(a[rt_], wn[nt_], zero4);
-                    } else {
-                        const float4v b = mfma(a[rt_], wf[SL][nt_].hi, zero4);
-                        return mfma(a[rt_], wf[SL][nt_].lo, b);
-                    }
+                    const float4v b = mfma(a[rt_], wf[SL][nt_].hi, zero4);
+                    return mfma(a[rt_], wf[SL][nt_].lo, b);
                 };
 #pragma unroll
                 for (int rt = 0; rt < RT; rt++)
@@ -716,34 +637,12 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
                         if (rt * NTW == t + 2) lds_a(rt);
                     if (t + 1 < T) blk[(t + 1) & 1] = blk_of((t + 1) / NTW, (t + 1) % NTW);
                     const int rt = t / NTW, nt = t % NTW;
-                    if constexpr (QN && QP_FOLD_PK) {
-                    // nibble weights: the fold on packed f32 (v_pk_mul / v_pk_fma; the
-                    // same per-element roundings as the scalar fold).  C5 A/B: 3-8 %
-                    // faster for W_Q4_1N, 7-12 % slower for the split planes.
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        float2v v = {acc[rt][nt][2 * h], acc[rt][nt][2 * h + 1]};
-                        float2v sc2 = TRANS ? float2v{da[rt][0], da[rt][0]} : float2v{da[rt][2 * h], da[rt][2 * h + 1]};
-                        if constexpr (QN)
-                            sc2 = sc2 * (TRANS ? float2v{dw[nt][2 * h], dw[nt][2 * h + 1]} : float2v{dw[nt][0], dw[nt][0]});
-                        v = __builtin_elementwise_fma(sc2, float2v{blk[t & 1][2 * h], blk[t & 1][2 * h + 1]}, v);
-                        if constexpr (QN1)  // + m_w s_a
-                            v = __builtin_elementwise_fma(float2v{dw[nt][1], dw[nt][1]}, float2v{sa[rt][2 * h], sa[rt][2 * h + 1]}, v);
-                        asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
-                        acc[rt][nt][2 * h] = v[0];
-                        acc[rt][nt][2 * h + 1] = v[1];
-                    }
-                    } else {
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         float v = acc[rt][nt][i];
-                        float sc_i = TRANS ? da[rt][0] : da[rt][i];
-                        if constexpr (QN) sc_i *= TRANS ? dw[nt][i] : dw[nt][0];
-                        v = __builtin_fmaf(sc_i, blk[t & 1][i], v);
-                        if constexpr (QN1) v = __builtin_fmaf(dw[nt][1], sa[rt][i], v);  // + m_w s_a
+                        v = __builtin_fmaf(TRANS ? da[rt][0] : da[rt][i], blk[t & 1][i], v);
                         asm volatile("" : "+v"(v));  // keep the fold here (no sinking past MFMAs)
                         acc[rt][nt][i] = v;
-                    }
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -793,7 +692,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
             for (int it = 0; it < IT; it++) {
                 int item = tid + it * NT;
                 asm volatile("" : "+v"(item));
-                if (item < ITEMS) a_store<AT, BM, LDA_H, KBT, QN1>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
+                if (item < ITEMS) a_store<AT, BM, LDA_H, KBT>(ar[it], smem + ((kc + 1) & 1) * A_BUF, item, unscale);
             }
         }
         __syncthreads();
@@ -807,7 +706,7 @@ __device__ __forceinline__ void gemm_mainloop(const GemmArgs &args, int64_t m0, 
     }
 }
 
-// X = (b + W.x) + X for the wave's column pairs (EPI_RESID, EPI_RESLN): lane
+// X = (b + W.x) + X for the wave's column pairs (EPI_RESID): lane
 // (g, c16), pair p, row tile rt, i: row m0 + 16 rt + 4 g + i, columns
 // colw + 32 p + {0, 1}
 template <int RT, int NP, int NTW>
@@ -836,21 +735,21 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
     constexpr int NTW = WN / 16;
     constexpr int NP = NTW / 2;  // column pairs per wave
     constexpr int RT = BM / 16;
-    constexpr bool QN1 = WT == W_Q4_1N, QN = WT == W_Q4_0N || QN1, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
-    constexpr int AT = act_of(WT);
+    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
+    constexpr int AT = WT;
     constexpr bool F32P = (WT == W_F32);
     constexpr int A_BYTES = F32P ? BM * LDA_F * 4 : BM * LDA_H * 2;
-    constexpr int A_BUF = A_BYTES + (QP ? (QN1 ? 2 : 1) * KB * BM * 4 : 0);
+    constexpr int A_BUF = A_BYTES + (QP ? KB * BM * 4 : 0);
     constexpr int ITEMS = BM * (KC / 16);            // 16-element A pieces per chunk
     constexpr int IT = (ITEMS + NT - 1) / NT;        // pieces per thread
     // Q4 / F16 GELU: transposed accumulators (Q4: in block-8 column order,
     // gemm_gelu_blk8), epilogue in registers; otherwise 16-row LDS slices
     constexpr bool GELU_T = (QP || WT == W_F16) && EPI == EPI_GELU_ACT;
     // LN: two 16-row slice buffers (stage + row partials) for BN <= 768
-    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || EPI == EPI_RESLN || GELU_T) ? 0 : (EPI == EPI_LN && BN <= 768 ? 2 : 1) * (16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0));
+    constexpr int EPI_LDS = (EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || GELU_T) ? 0 : (EPI == EPI_LN && BN <= 768 ? 2 : 1) * (16 * (BN + 4) * 4 + ((EPI == EPI_LN) ? 2 * 16 * (BN / 32) * 8 : 0));
     constexpr int SMEM = (2 * A_BUF > EPI_LDS) ? 2 * A_BUF : EPI_LDS;
     static_assert(NTW % 2 == 0, "wave tile must hold whole column pairs");
-    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || EPI == EPI_RESLN || (BN / 32) % NW == 0,
+    static_assert(EPI == EPI_QKV || EPI == EPI_NONE || EPI == EPI_RESID || (BN / 32) % NW == 0,
                   "epilogue: whole quarter-tasks per thread");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
     constexpr bool GT_LDS = EPI == EPI_GELU_ACT;
@@ -936,38 +835,6 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         return;
     }
 
-    if constexpr (EPI == EPI_RESLN) {
-        // One workgroup per BM-row tile walks all n_ntiles column tiles:
-        // X = (b + W.x) + X as EPI_RESID, then LayerNorm of the tile's rows in
-        // place from its own just-written X (same CU: the barrier orders the
-        // other waves' stores before the loads) with ln_rows16 — bitwise the
-        // EPI_RESID + launch_ln pair, without the LN pass's re-read of X from
-        // HBM and its launch (rows too wide for one workgroup's tile: n_embd 768
-        // and 1024 on the Q4 split weights).
-        const int64_t mr = (int64_t)blockIdx.x * BM;
-        for (int nt = 0; nt < n_ntiles; nt++) {
-            const int64_t nt0 = ((int64_t)nt * BN + wv * WN) >> 4;
-            float4v acc[RT][NTW];
-            {
-                MainloopPre<WT, NW, BM, NTW> pre;
-                mainloop_preload(pre, args, mr, nt0);
-                gemm_mainloop<WT, NW, BM, NTW, false>(args, mr, nt0, smem, acc, pre);
-            }
-            resid_epilogue<RT, NP>(args, mr, nt * BN + wv * WN + 2 * c16, acc);
-        }
-        __syncthreads();
-        constexpr int LT = act_of(WT);
-        double *red = (double *)smem;
-        float *stat = (float *)(red + 16 * 32);
-        static_assert(16 * 32 * 8 + 16 * 4 <= SMEM, "LN partials fit the A buffers");
-        for (int r16 = 0; r16 < BM; r16 += 16) {
-            if (args.N == 1024)
-                ln_rows16<LT, 32, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, mr + r16, red, stat);
-            else
-                ln_rows16<LT, 24, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, mr + r16, red, stat);
-        }
-        return;
-    }
     int64_t m0;
     int n0;
     tile_of(blockIdx.x, m0, n0);
@@ -1217,14 +1084,7 @@ __device__ __forceinline__ void attn_store_ctx(const AttnArgs &a, float16v *o, f
 #pragma unroll
         for (int j = 0; j < 16; j++) o[dt][j] *= rs;
         const int col0 = h * D + (dt0 + dt) * 32;
-        if constexpr (WT == W_Q4_0D) {
-            // the lane pair's 32 values are one Q8D block, in its position order
-            float y[16];
-#pragma unroll
-            for (int j = 0; j < 16; j++) y[j] = o[dt][j];
-            const int64_t bi = row * (E >> 5) + (col0 >> 5);
-            q8d_store_pair((char *)a.ctx.q + bi * Q8D_BLK, (uint16_t *)a.ctx.d + bi, hh, y, valid);
-        } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+        if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
             float amax = 0.f;
 #pragma unroll
             for (int j = 0; j < 16; j++) amax = fmaxf(amax, fabsf(o[dt][j]));
@@ -1414,7 +1274,7 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 // never leave the CU — the unfused pair writes and re-reads 12 bytes per
 // token and feature.  The QKV features go through the GEMM main loop in
 // 192-feature units (a head pair at D = 32, one head at D = 64), NTW units per
-// main loop (qkv_attention_ntw) and one unit at a time through the attention
+// main loop (ntw, chosen per context at load) and one unit at a time through the attention
 // tiles: the main loop (gemm_mainloop, the 128 rows from the sentence's first
 // token) computes the unit's head-major QKV features (kernels.h GemmArgs), one
 // 16-feature n-tile per wave; b + W.x is split hi/lo into the unit's attention
@@ -1426,26 +1286,19 @@ constexpr int QKVA_NW = 12;  // waves
 #ifndef QKVA_KB
 #define QKVA_KB 2  // 32-wide blocks per main-loop chunk in the fused kernel
 #endif
-// A/B (-DQKVA_KEEP_S=1): the fused kernel's attention keeps its (<= 4) score
-// tiles in registers between the max pass and the probability pass instead of
-// recomputing them.  Measured: with two units per main loop it spills (the
-// second unit's accumulators are live) and runs 360 -> 463 us; with one unit
-// per main loop (BERT_AMD_QKVA_NTW=1) 410 -> 413 us, i.e. the 37.5 % fewer
-// attention MFMAs buy nothing: the attention phase is not MFMA-bound.
-#ifndef QKVA_KEEP_S
-#define QKVA_KEEP_S 0
-#endif
+// (Keeping the <= 4 score tiles in registers between the max pass and the
+// probability pass instead of recomputing them measured 360 -> 463 us with two
+// units per main loop (spills) and 410 -> 413 us with one: the attention
+// phase is not MFMA-bound)
 // (Software-pipelined score tiles in the attention phase — tile kt + 1's K.Q
 // MFMAs in flight during tile kt's softmax — measured 368 -> 392-399 us with
 // 28 B/lane of spills: not kept.)
 
-// D: head dim; NTW: 192-feature units per main loop (qkv_attention_ntw); PK:
+// D: head dim; NTW: 192-feature units per main loop (ntw); PK:
 // sentence tiles (a.tiles)
-// CT: the context's activation format (WT, or W_Q4_0D: Q4_0 weights read from
-// int8 Q8_0 activations, context stored as Q8D for the fp6 O projection)
-template <int WT, int D, int NTW, bool PK, int CT = WT>
+template <int WT, int D, int NTW, bool PK>
 __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g, AttnArgs a) {
-    constexpr bool QN = WT == W_Q4_0N, QP = (WT == W_Q4_0 || WT == W_Q4_1 || QN);
+    constexpr bool QP = (WT == W_Q4_0 || WT == W_Q4_1);
     constexpr int NW = QKVA_NW, BM = 128, RT = BM / 16;
     constexpr int HU = 192 / (3 * D);  // heads per unit
     constexpr int NK = 128, KST = D + 8, VST = NK + 4;
@@ -1641,25 +1494,11 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                         return S;
                     };
                     float mx = -INFINITY;
-#if QKVA_KEEP_S
-                    // the key tiles' scores stay in registers for pass 2 (n <= 128: at
-                    // most 4 tiles), so each score tile is computed once
-                    float16v Sk[4];
-#pragma unroll
-                    for (int kt = 0; kt < 4; kt++) {
-                        if (kt < nkt) {
-                            Sk[kt] = scores(kt);
-#pragma unroll
-                            for (int j = 0; j < 16; j++) mx = fmaxf(mx, Sk[kt][j]);
-                        }
-                    }
-#else
                     for (int kt = 0; kt < nkt; kt++) {
                         const float16v S = scores(kt);
 #pragma unroll
                         for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
                     }
-#endif
                     mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
                     const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
                     // ggml's double sum of the fp16 probabilities, exactly: every p is a
@@ -1668,15 +1507,8 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     uint32_t sum = 0;
                     float16v o[1];
                     o[0] = float16v{};
-#if QKVA_KEEP_S
-#pragma unroll
-                    for (int kt = 0; kt < 4; kt++) {
-                        if (kt >= nkt) continue;
-                        const float16v S = Sk[kt];
-#else
                     for (int kt = 0; kt < nkt; kt++) {
                         const float16v S = scores(kt);
-#endif
                         half8 ph[2];
 #pragma unroll
                         for (int j = 0; j < 16; j += 2) {
@@ -1701,7 +1533,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                     sum += __shfl_xor(sum, 32);
                     int orow = qrow;
                     asm volatile("" : "+v"(orow));
-                    attn_store_ctx<CT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, head,
+                    attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, head,
                                              hh, dh);
                 }
             }
@@ -1710,42 +1542,30 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     }
 }
 
-template <int WT, int D, int CT>
-static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
+template <int WT, int D>
+static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s) {
     const bool pk = a.tiles != nullptr;
-    if (qkv_attention_ntw(WT) == 2) {
+    if (ntw == 2) {
         if (pk)
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, true, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
         else
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, false, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
     } else {
         if (pk)
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, true, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
         else
-            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, false, CT>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
+            hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 1, false>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
     }
     return hipGetLastError();
 }
 
-template <int WT, int CT = WT>
-static hipError_t qkv_attn_w(const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
+template <int WT>
+static hipError_t qkv_attn_w(const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s) {
     switch (a.H > 0 ? a.E / a.H : 0) {
-        case 32: return qkv_attn_t<WT, 32, CT>(g, a, n_blocks, s);
-        case 64: return qkv_attn_t<WT, 64, CT>(g, a, n_blocks, s);
+        case 32: return qkv_attn_t<WT, 32>(g, a, n_blocks, ntw, s);
+        case 64: return qkv_attn_t<WT, 64>(g, a, n_blocks, ntw, s);
     }
     return hipErrorInvalidValue;
-}
-
-// Head pairs per main loop: two (one pass over a sentence's A panel serves
-// four heads).  Env BERT_AMD_QKVA_NTW=1 selects one pair per pass (A/B
-// checks; tools/qkva_check.hip compares the two bitwise).
-int qkv_attention_ntw(int wtype) {
-    (void)wtype;
-    static const int ntw = [] {
-        const char *e = std::getenv("BERT_AMD_QKVA_NTW");
-        return e && std::atoi(e) == 1 ? 1 : 2;
-    }();
-    return ntw;
 }
 
 static int n_cus() {
@@ -1768,22 +1588,19 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles) {
     return n_tiles < n_seqs && packed * 11 < plain * 10;
 }
 
-bool qkv_attention_supported(int wtype, int E, int H, int max_len) {
-    if (H <= 0 || E % H) return false;
+bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw) {
+    if (H <= 0 || E % H || (ntw != 1 && ntw != 2)) return false;
     const int D = E / H;
-    return max_len <= 128 && (D == 32 || D == 64) && H % (192 / (3 * D) * qkv_attention_ntw(wtype)) == 0 &&
-           E % KC == 0 && wtype != W_F32;
+    return max_len <= 128 && (D == 32 || D == 64) && H % (192 / (3 * D) * ntw) == 0 && E % KC == 0 &&
+           wtype != W_F32;
 }
 
-hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, hipStream_t s) {
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s) {
+    if (!qkv_attention_supported(wtype, a.E, a.H, 0, ntw)) return hipErrorInvalidValue;
     switch (wtype) {
-        case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, s);
-        case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, s);
-        case W_Q4_0D: return qkv_attn_w<W_Q4_0, W_Q4_0D>(g, a, n_blocks, s);
-        case W_Q4_0N:
-            if (g.K < 32 * w_ring(W_Q4_0N)) return hipErrorInvalidValue;
-            return qkv_attn_w<W_Q4_0N, W_Q4_0>(g, a, n_blocks, s);
-        case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, s);
+        case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, ntw, s);
+        case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, ntw, s);
+        case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, ntw, s);
     }
     return hipErrorInvalidValue;
 }
@@ -1799,11 +1616,6 @@ hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a,
 // softmax VALU and the chunk loads are amortised over 256 queries.
 constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, queries per workgroup
 
-// development ablations (timing only, wrong results): 1 = no K / V global
-// loads (zeros staged), 2 = no pass-1 score tiles
-#ifndef ATTN_LONG_ABL
-#define ATTN_LONG_ABL 0
-#endif
 #ifndef ATTN_LONG_KT_UNROLL
 #define ATTN_LONG_KT_UNROLL(D) 1  // A/B: -D'ATTN_LONG_KT_UNROLL(D)=4' (the round-2 form)
 #endif
@@ -1849,7 +1661,7 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, D == 32 ? 4 : 1) void attention_
         for (int i = 0; i < KIT; i++) {
             const int idx = tid + NT * i, key = idx / (D / 8), col = (idx - key * (D / 8)) * 8;
             pkh[i] = pkl[i] = uint4{0u, 0u, 0u, 0u};
-            if (!(ATTN_LONG_ABL & 1) && kbase + key < n) {
+            if (kbase + key < n) {
                 const int64_t off = (int64_t)(beg + kbase + key) * E2 + E + h * D + col;
                 pkh[i] = *(const uint4 *)(a.qk_hi + off);
                 pkl[i] = *(const uint4 *)(a.qk_lo + off);
@@ -1861,7 +1673,6 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, D == 32 ? 4 : 1) void attention_
             const int idx = tid + NT * i, d = idx / (NK / 8), k8 = (idx - d * (NK / 8)) * 8;
             const int64_t off = (int64_t)(h * D + d) * a.ldv + beg + kbase + k8;
             pvh[i] = pvl[i] = half8{};
-            if (ATTN_LONG_ABL & 1) continue;
             if (kbase + k8 + 8 <= n && v_aligned) {
                 pvh[i] = *(const half8 *)(a.vt_hi + off);
                 pvl[i] = *(const half8 *)(a.vt_lo + off);
@@ -1931,7 +1742,6 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, D == 32 ? 4 : 1) void attention_
         // (Software-pipelining the score tiles — the next tile's K.Q MFMAs issued
         // before this tile's softmax — measured 1 - 3 % slower: not kept.)
         constexpr int KTU = ATTN_LONG_KT_UNROLL(D);
-        if ((ATTN_LONG_ABL & 2) && !p2) continue;
 #pragma unroll KTU
         for (int kt = 0; kt < NK / 32; kt++) {
             const int k0 = c * NK + 32 * kt;
@@ -2044,7 +1854,6 @@ hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s) 
         case W_F16: return embed_t<W_F16>(a, Mpad, s);
         case W_Q4_0: return embed_t<W_Q4_0>(a, Mpad, s);
         case W_Q4_1: return embed_t<W_Q4_1>(a, Mpad, s);
-        case W_Q4_0D: return embed_t<W_Q4_0D>(a, Mpad, s);
     }
     return hipErrorInvalidValue;
 }
@@ -2061,7 +1870,7 @@ static bool ln_half_rows(int Mpad) {
 template <int WT, int EPI, int BN, int NW, int BM>
 static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
     const int mt = Mpad / BM, nt = a.N / BN;
-    int grid = EPI == EPI_RESLN ? mt : mt * nt;  // EPI_RESLN: a workgroup walks a row tile's n-tiles
+    int grid = mt * nt;
     if constexpr ((WT == W_Q4_0 || WT == W_Q4_1 || WT == W_F16) && EPI == EPI_GELU_ACT) {
         // persistent: one workgroup per CU (the GELU table fills the LDS), a multiple of 8
         if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS) return hipErrorInvalidValue;
@@ -2077,15 +1886,7 @@ static hipError_t gemm_t(const GemmArgs &a, int Mpad, hipStream_t s) {
 // 64 rows.  LayerNorm GEMMs own whole rows (BN = E).
 template <int WT>
 static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
-    if constexpr (WT == W_Q4_0N || WT == W_Q4_1N) {  // nibble weights: QKV (unfused), O / down (+ LN or residual)
-        if (a.K < 32 * w_ring(WT)) return hipErrorInvalidValue;  // the ring's preload reads w_ring blocks
-        if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
-        if (epi == EPI_LN && a.N == 384)
-            return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
-                                      : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
-        if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
-        if (epi == EPI_RESLN) return gemm_t<WT, EPI_RESLN, 256, 8, 128>(a, Mpad, s);
-    } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         if (epi == EPI_QKV) return gemm_t<WT, EPI_QKV, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_GELU_ACT)  // 12 waves (3 per SIMD) where N allows; the GELU table fills the LDS
             return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)
@@ -2094,7 +1895,6 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
             return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
                                       : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
-        if (epi == EPI_RESLN) return gemm_t<WT, EPI_RESLN, 256, 8, 128>(a, Mpad, s);
     } else if constexpr (WT == W_F16) {
         // tools/gemm_bench (e5 shapes): 12-wave 384-column tiles win by 1.3-1.8x over
         // 4-6 waves and by 11-14 % over 768 x 64 tiles (qkv 343 us, up+GELU 368 us)
@@ -2135,7 +1935,6 @@ bool gemm_shape_supported(int epi, int N, int K) {
     if (K % KC) return false;
     if (epi == EPI_QKV) return N % 384 == 0;
     if (epi == EPI_GELU_ACT || epi == EPI_RESID) return N % 256 == 0;
-    if (epi == EPI_RESLN) return N == 768 || N == 1024;  // Q4 split / nibble weights only (gemm_w)
     return N == 384 || N == 768 || N == 1024;
 }
 
@@ -2146,8 +1945,6 @@ hipError_t launch_gemm(int wtype, int epi, int /*unused*/, const GemmArgs &a, in
         case W_F16: return gemm_w<W_F16>(epi, a, Mpad, s);
         case W_Q4_0: return gemm_w<W_Q4_0>(epi, a, Mpad, s);
         case W_Q4_1: return gemm_w<W_Q4_1>(epi, a, Mpad, s);
-        case W_Q4_0N: return gemm_w<W_Q4_0N>(epi, a, Mpad, s);
-        case W_Q4_1N: return gemm_w<W_Q4_1N>(epi, a, Mpad, s);
     }
     return hipErrorInvalidValue;
 }
@@ -2180,7 +1977,6 @@ hipError_t launch_attention(int wtype, int d_head, const AttnArgs &a, int n_seqs
         case W_F16: return attn_w<W_F16>(d_head, a, n_seqs, max_len, s);
         case W_Q4_0: return attn_w<W_Q4_0>(d_head, a, n_seqs, max_len, s);
         case W_Q4_1: return attn_w<W_Q4_1>(d_head, a, n_seqs, max_len, s);
-        case W_Q4_0D: return attn_w<W_Q4_0D>(d_head, a, n_seqs, max_len, s);
     }
     return hipErrorInvalidValue;
 }
@@ -2204,7 +2000,6 @@ hipError_t launch_ln(int wtype, float *X, int Mpad, int E, const float *w, const
         case W_F16: return ln_w<W_F16>(X, Mpad, E, w, b, eps, out, s);
         case W_Q4_0: return ln_w<W_Q4_0>(X, Mpad, E, w, b, eps, out, s);
         case W_Q4_1: return ln_w<W_Q4_1>(X, Mpad, E, w, b, eps, out, s);
-        case W_Q4_0D: return ln_w<W_Q4_0D>(X, Mpad, E, w, b, eps, out, s);
     }
     return hipErrorInvalidValue;
 }

@@ -57,129 +57,12 @@ __device__ __forceinline__ void q8_scales(float amax, float &d, float &id) {
 }
 
 // ---------------------------------------------------------------------------
-// Q8D (kernels.h W_Q4_0D): the Q8_0 block (d, q[32]) of ggml's quantiser,
-// stored as the two fp6 (e2m3) digit planes the block-scaled MFMA consumes
-// (gemm_f6.hip).  q = 16 H + L with H = trunc(q / 16), L = q - 16 H (both
-// carry q's sign, |H| <= 7, |L| <= 15); a digit v is stored as the e2m3 code
-// of v / 8 (= sign << 5 | |v|: under the MFMA's 2^3 scale e2m3 holds every
-// integer of [-16, 16]).  Block element e sits at plane position q8d_pos(e)
-// (6-bit field at bit 6 p), the order in which v_cvt_scalef32_2xpk16_fp6_f32
-// interleaves its two inputs (position 2 i <- a[i], 2 i + 1 <- b[i];
-// tools/cvt_fp6_probe.hip) when a[i], b[i] are the two lanes of a 32 x 32 MFMA
-// result pair holding element (i & 3) + 8 (i >> 2) + 4 hh:
-//   q8d_pos(e) = 8 (e >> 3) + 2 (e & 3) + ((e >> 2) & 1)
-// (eight consecutive elements 8 k .. 8 k + 7 fill positions 8 k .. 8 k + 7).
-__device__ __host__ __forceinline__ int q8d_pos(int e) { return 8 * (e >> 3) + 2 * (e & 3) + ((e >> 2) & 1); }
-
-typedef int q8d_i32x6 __attribute__((ext_vector_type(6)));
-typedef float q8d_f32x16 __attribute__((ext_vector_type(16)));
-
-// Block layout (48 bytes): hi plane bytes 0-15 | lo 0-15 | hi 16-23 | lo 16-23,
-// so each MFMA lane half reads 16 + 8 aligned bytes (at 16 hh and 32 + 8 hh).
-// Plane byte n of block `blk`:
-__device__ __forceinline__ char *q8d_byte(char *blk, int plane, int n) {
-    return blk + (n < 16 ? 16 * plane + n : 32 + 8 * plane + (n - 16));
-}
-
-// Digits of q = rint(y * id) (ggml: the product rounded to f32, then to an
-// integer, half to even)
-__device__ __forceinline__ void q8d_digits(float y, float id, float &h, float &l) {
-    const float q = __builtin_rintf(y * id);
-    h = __builtin_truncf(q * 0.0625f);
-    l = __builtin_fmaf(-16.0f, h, q);
-}
-
-// One Q8 block held as 16 values by each of the lanes l and l ^ 32 (same
-// row), lane half hh holding elements (i & 3) + 8 (i >> 2) + 4 hh: amax over
-// the pair, ggml's d / id, digits; the pair swaps digits (half 0 gathers the
-// H plane, half 1 the L plane) and each lane converts and stores one whole
-// plane.  `blk` is the block's 48 bytes.
-__device__ __forceinline__ void q8d_store_pair(char *blk, uint16_t *dptr, int hh, const float (&y)[16],
-                                               bool valid = true) {
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; i++) amax = fmaxf(amax, fabsf(y[i]));
-    {
-        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
-        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
-    }
-    float d, id;
-    q8_scales(amax, d, id);
-    q8d_f32x16 a, b;
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        float h, l;
-        q8d_digits(y[i], id, h, l);
-        // lanes 0-31 keep h and receive the partner's h; lanes 32-63 keep l and receive the partner's l
-        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(h), __float_as_uint(l), false, false);
-        a[i] = __uint_as_float(s[0]);
-        b[i] = __uint_as_float(s[1]);
-    }
-    const q8d_i32x6 c = __builtin_amdgcn_cvt_scalef32_2xpk16_fp6_f32(a, b, 8.0f);
-    if (valid) {
-        *(uint4 *)(blk + 16 * hh) = make_uint4(c[0], c[1], c[2], c[3]);
-        *(uint2 *)(blk + 32 + 8 * hh) = make_uint2(c[4], c[5]);
-        if (hh == 0) *dptr = f2h(d);
-    }
-}
-
-// Eight consecutive elements 8 qq .. 8 qq + 7 of a block (the quarter
-// producers): plane positions 8 qq .. 8 qq + 7, i.e. plane bytes 6 qq ..
-// 6 qq + 5 of both planes, from one conversion (bits 0-47: H, 48-95: L).
-__device__ __forceinline__ void q8d_store_quarter(char *blk, int qq, const float (&v)[8], float id) {
-    q8d_f32x16 a, b;
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        float h, l;
-        q8d_digits(v[t], id, h, l);
-        a[t] = h;
-        a[4 + t] = l;
-        q8d_digits(v[4 + t], id, h, l);
-        b[t] = h;
-        b[4 + t] = l;
-    }
-#pragma unroll
-    for (int t = 8; t < 16; t++) a[t] = b[t] = 0.f;
-    const q8d_i32x6 c = __builtin_amdgcn_cvt_scalef32_2xpk16_fp6_f32(a, b, 8.0f);
-    const uint32_t h0 = (uint32_t)c[0], h1 = (uint32_t)c[1] & 0xffffu;
-    const uint32_t l0 = (uint32_t)c[1] >> 16 | (uint32_t)c[2] << 16, l1 = (uint32_t)c[2] >> 16;
-    // 6 bytes at plane byte 6 qq: a dword and a short, split where the block layout does
-#pragma unroll
-    for (int pl = 0; pl < 2; pl++) {
-        const uint32_t w0 = pl ? l0 : h0, w1 = pl ? l1 : h1;
-        const int n = 6 * qq;
-        if ((qq & 1) == 0) {  // bytes n .. n + 3 | n + 4 .. n + 5
-            *(uint32_t *)q8d_byte(blk, pl, n) = w0;
-            *(uint16_t *)q8d_byte(blk, pl, n + 4) = (uint16_t)w1;
-        } else {  // bytes n .. n + 1 | n + 2 .. n + 5
-            *(uint16_t *)q8d_byte(blk, pl, n) = (uint16_t)w0;
-            *(uint32_t *)q8d_byte(blk, pl, n + 2) = w0 >> 16 | w1 << 16;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Activation block store: one 32-element block of one row, in the format the
 // next matmul consumes (ggml quantize_row_q8_0 / q8_1 AVX2 semantics:
 // d = amax/127, q = rint(x * (127/amax)); fp16 RNE; or f32).
 template <int WT>
 __device__ __forceinline__ void store_act_block(const ActPtr &A, int64_t ld, int64_t row, int blk, const float *v) {
-    if constexpr (WT == W_Q4_0D) {
-        float amax = 0.f;
-#pragma unroll
-        for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(v[j]));
-        float d, id;
-        q8_scales(amax, d, id);
-        char *b = (char *)A.q + (row * (ld / 32) + blk) * Q8D_BLK;
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            float w[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) w[j] = v[8 * qq + j];
-            q8d_store_quarter(b, qq, w, id);
-        }
-        ((uint16_t *)A.d)[row * (ld / 32) + blk] = f2h(d);
-    } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         float amax = 0.f;
 #pragma unroll
         for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(v[j]));
@@ -218,20 +101,7 @@ __device__ __forceinline__ void store_act_block(const ActPtr &A, int64_t ld, int
 template <int WT>
 __device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, int64_t row, int blk, int qq,
                                                   const float *v) {
-    if constexpr (WT == W_Q4_0D) {
-        float amax = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
-        amax = fmaxf(amax, __shfl_xor(amax, 1));
-        amax = fmaxf(amax, __shfl_xor(amax, 2));
-        float d, id;
-        q8_scales(amax, d, id);
-        float w[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) w[j] = v[j];
-        q8d_store_quarter((char *)A.q + (row * (ld / 32) + blk) * Q8D_BLK, qq, w, id);
-        if (qq == 0) ((uint16_t *)A.d)[row * (ld / 32) + blk] = f2h(d);
-    } else if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
+    if constexpr (WT == W_Q4_0 || WT == W_Q4_1) {
         float amax = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
@@ -268,28 +138,7 @@ __device__ __forceinline__ void store_act_quarter(const ActPtr &A, int64_t ld, i
 template <int WT>
 __device__ __forceinline__ void store_act_quarter_t(const ActPtr &A, int64_t ld, int64_t row, int blk, int qq,
                                                     const float *v) {
-    static_assert(WT == W_Q4_0 || WT == W_Q4_1 || WT == W_Q4_0D, "Q8 activation formats only");
-    if constexpr (WT == W_Q4_0D) {
-        float amax = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
-        {
-            const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
-            amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
-        }
-        {
-            const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
-            amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
-        }
-        float d, id;
-        q8_scales(amax, d, id);
-        float w[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) w[j] = v[j];
-        q8d_store_quarter((char *)A.q + (row * (ld / 32) + blk) * Q8D_BLK, qq, w, id);
-        if (qq == 0) ((uint16_t *)A.d)[row * (ld / 32) + blk] = f2h(d);
-        return;
-    }
+    static_assert(WT == W_Q4_0 || WT == W_Q4_1, "Q8 activation formats only");
     float amax = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -176,8 +177,6 @@ struct DevMat {
 struct DevLayer {
     WPtr qkv, o, up, down;
     I8W o8, up8, down8;  // Q4 weights for the int8-MFMA GEMMs (gemm_i8.hip)
-    I8W ffn8;            // both FFN projections as the fused kernel's stream (upload_ffn_i8)
-    F6W o6, up6, down6;  // Q4_0 weights for the fp6-MFMA GEMMs (gemm_f6.hip)
     WPtr qkv_plain;  // head-major QKV in grouped, plain tile order: qkv_attention_kernel's copy (when supported)
     float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
@@ -189,7 +188,6 @@ struct Workspace {
     float *X = nullptr, *out = nullptr;
     uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16: kernels.h GemmArgs EPI_QKV
     ActPtr Xa, Ca, Ua;
-    ActPtr Xd;  // fp6 path: the O + LN output as Q8D (the FFN-up GEMM's input; Xa keeps ggml's Q8_0 for QKV)
     int32_t *tok = nullptr, *off = nullptr, *rowpos = nullptr;
     int32_t *tiles = nullptr;  // qkv_attention_kernel's sentence tiles: [first, count] pairs
     int32_t *perm = nullptr;   // eval_device in tile order: caller's index of each sentence
@@ -259,23 +257,19 @@ struct bert_ctx {
     std::vector<std::unique_ptr<Replica>> reps;
     // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
     bool i8_o = false, i8_up = false, i8_down = false;
-    // Q4_0 models whose O / FFN GEMMs run on the fp6 MFMA (gemm_f6.hip): their
-    // activations are stored as Q8D (kernels.h W_Q4_0D); f6_select
-    bool f6 = false;
-    // Q4_0 QKV (fused and unfused) and split-path O weights as nibbles,
-    // dequantised inside the fp16 MFMA GEMM (kernels.h W_Q4_0N); nib_select
-    bool q4nib = false;
-    // FFN-up + GELU + FFN-down + LN in one kernel (gemm_i8.hip i8_ffn384_kernel;
-    // ffn_select): ffn_ok = its weight stream is uploaded, ffn_fused = in use
-    bool ffn_ok = false, ffn_fused = false;
-    // run_pipeline knobs, read from the environment once at load
-    // (BERT_AMD_SPLIT, BERT_AMD_PACK) and changed only by bert_amd_set_option:
+    // 192-feature units per main loop of the fused QKV + attention kernel (1 or
+    // 2): the tile grouping of its QKV weight copy, fixed at load
+    int qkva_ntw = 2;
+    // run_pipeline knobs: defaults, then the load options (LoadOpts), then
+    // bert_amd_set_option; nothing is read from the environment after load.
+    // unfused: every batch on the QKV GEMM + attention pair (A/B checks);
     // two row groups on two streams (default on); fused-tile packing
     // -1 = when it pays (default), 0 = never, 1 = always; batches of fewer than
     // fuse_min sentences skip the fused QKV + attention kernel (one workgroup per
     // sentence: its latency, not the chip, bounds a small batch) for the unfused
     // pair, whose GEMM and attention spread a sentence over many workgroups
     int split = 1, pack = -1, fuse_min = 48;
+    bool unfused = false;
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
     // merging only up to encode_merge_rows sentences (slices that large already
@@ -285,13 +279,6 @@ struct bert_ctx {
     // lanes x merge 1 x 1 12 k emb/s, 4 x 1 35-56 k, 2 x 4 101 k, 4 x 4 109 k,
     // 8 x 4 92 k, 6 x 8 124 k, 4 x 8 173 k, 2 x 16 184 k (device-resident 265 k)
     int encode_lanes = 2, encode_merge = 16, encode_merge_rows = 256;
-    // Q4 models wider than 384 (LN rows wider than one GEMM tile): the O and
-    // FFN-down residual GEMMs can normalise their rows in the same kernel
-    // (EPI_RESLN: one workgroup walks a row tile's column tiles, then LN) instead
-    // of EPI_RESID + launch_ln; bitwise the same.  Opt-in (env BERT_AMD_RESLN=1
-    // or option "resln"): measured slower on C5 (the in-kernel LN
-    // phase is exposed, one 8-wave workgroup per CU).
-    bool resln = false;
     std::mutex mu;  // one eval at a time per context (the reference ctx is not re-entrant either)
 };
 
@@ -320,7 +307,7 @@ struct Packed {
     float unscale = 1.f;
 };
 
-Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_t K, bool nib = false) {
+Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_t K) {
     const int64_t N = (int64_t)rows_in.size(), nkb = K / 32, ntl = N / 16;
     // column interleave (kernels.h WPtr): repacked tile 2p+t, lane column c
     // <- weight row 32p + 2c + t, i.e. repacked row 16*(2p+t) + c
@@ -329,60 +316,7 @@ Packed repack(uint32_t type, const std::vector<const uint8_t *> &rows_in, int64_
         for (int t = 0; t < 2; t++)
             for (int c = 0; c < 16; c++) rows[(size_t)(32 * pr + 16 * t + c)] = rows_in[(size_t)(32 * pr + 2 * c + t)];
     Packed p;
-    if (nib && type == GT_Q4_1) {
-        // kernels.h W_Q4_1N: per (n-tile, block) and lane (c, g) one 8-byte
-        // record {8 nibbles q of row c, k = 8 g + j at bits 4 (j >> 1) + 16 (j & 1);
-        // fp16 d | m << 16 of row c}
-        p.q.resize((size_t)(ntl * nkb * 64 * 8));
-        uint32_t *q = (uint32_t *)p.q.data();
-        for (int64_t nt = 0; nt < ntl; nt++)
-            for (int64_t kb = 0; kb < nkb; kb++)
-                for (int lane = 0; lane < 64; lane++) {
-                    const int c = lane & 15, g = lane >> 4;
-                    const uint8_t *blk = rows[(size_t)(nt * 16 + c)] + kb * 20;
-                    uint32_t x = 0;
-                    for (int j = 0; j < 8; j++) {
-                        const int e = 8 * g + j;
-                        const uint8_t byte = blk[4 + (e & 15)];
-                        const uint32_t qv = e < 16 ? (byte & 15u) : (byte >> 4);
-                        x |= qv << (4 * (j >> 1) + 16 * (j & 1));
-                    }
-                    uint32_t *r = &q[(size_t)(((nt * nkb + kb) * 64 + lane) * 2)];
-                    r[0] = x;
-                    std::memcpy(&r[1], blk, 4);  // d, m (fp16, little-endian: d in the low half)
-                }
-        p.unscale = 1.f;
-    } else if (nib && type == GT_Q4_0) {
-        // kernels.h W_Q4_0N: per (n-tile, block) and lane (c, g) one 16-byte
-        // record {8 nibbles of row c, k = 8 g + j at bits 4 (j >> 1) + 16 (j & 1);
-        // fp16 d of rows 4g .. 4g + 3; fp16 d of row c}
-        p.q.resize((size_t)(ntl * nkb * 64 * 16));
-        uint32_t *q = (uint32_t *)p.q.data();
-        auto dh = [&](int64_t row, int64_t kb) {
-            uint16_t v;
-            std::memcpy(&v, rows[(size_t)row] + kb * 18, 2);
-            return (uint32_t)v;
-        };
-        for (int64_t nt = 0; nt < ntl; nt++)
-            for (int64_t kb = 0; kb < nkb; kb++)
-                for (int lane = 0; lane < 64; lane++) {
-                    const int c = lane & 15, g = lane >> 4;
-                    const uint8_t *blk = rows[(size_t)(nt * 16 + c)] + kb * 18;
-                    uint32_t x = 0;
-                    for (int j = 0; j < 8; j++) {
-                        const int e = 8 * g + j;
-                        const uint8_t byte = blk[2 + (e & 15)];
-                        const uint32_t qv = e < 16 ? (byte & 15u) : (byte >> 4);
-                        x |= qv << (4 * (j >> 1) + 16 * (j & 1));
-                    }
-                    uint32_t *r = &q[(size_t)(((nt * nkb + kb) * 64 + lane) * 4)];
-                    r[0] = x;
-                    r[1] = dh(nt * 16 + 4 * g, kb) | dh(nt * 16 + 4 * g + 1, kb) << 16;
-                    r[2] = dh(nt * 16 + 4 * g + 2, kb) | dh(nt * 16 + 4 * g + 3, kb) << 16;
-                    r[3] = dh(nt * 16 + c, kb);
-                }
-        p.unscale = 1.f;
-    } else if (type == GT_Q4_0 || type == GT_Q4_1) {
+    if (type == GT_Q4_0 || type == GT_Q4_1) {
         // w = d*(q-8) | d*q + m, exact in double; scaled by 2^S so that
         // max|w| lands in [2^13, 2^14): the fp16 hi part stays far from
         // overflow and the lo part stays normal for all but negligible weights
@@ -526,83 +460,6 @@ bool upload_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vec
     return upload_i8w(track, w, repack_i8(type, rows, K));
 }
 
-// The fused FFN kernel's weight stream (gemm_i8.hip i8_ffn384_kernel): for
-// each of the 12 waves, the int8 fragments of the blocks it reads in its
-// per-tile order (slices j = 0 .. I/384 - 1: up_j = 12 blocks of up f-tile
-// 12 j + w, then down_j = blocks 12 j .. 12 j + 11 of down f-tile w),
-// contiguous, and the chunk scale vectors (4 blocks) in the same order — the
-// same values as upload_i8's, so the kernel's loads are linear in the sequence.
-bool upload_ffn_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vector<const uint8_t *> &up_rows,
-                   const std::vector<const uint8_t *> &down_rows, int64_t E, int64_t I) {
-    const I8Host U = repack_i8(type, up_rows, E), D = repack_i8(type, down_rows, I);
-    const int64_t nj = I / 384, qt = 24 * nj, ct = 6 * nj, nkbu = E / 32, nkbd = I / 32;
-    const bool q1 = type == GT_Q4_1;
-    I8Host S;
-    S.q.resize((size_t)(12 * qt * 64 * 16));
-    S.d.resize((size_t)(12 * ct * 32 * 4));
-    if (q1) S.m.resize(S.d.size());
-    else S.dh.resize(S.d.size());
-    for (int64_t wv = 0; wv < 12; wv++) {
-        for (int64_t q = 0; q < qt; q++) {
-            const int64_t p = q / 12, b = q % 12, j = p / 2;
-            const int8_t *src = (p & 1) ? &D.q[(size_t)((wv * nkbd + 12 * j + b) * 64 * 16)]
-                                        : &U.q[(size_t)(((12 * j + wv) * nkbu + b) * 64 * 16)];
-            std::memcpy(&S.q[(size_t)((wv * qt + q) * 64 * 16)], src, 64 * 16);
-        }
-        for (int64_t c = 0; c < ct; c++) {
-            const int64_t p = c / 3, cc = c % 3, j = p / 2;
-            const bool dn = p & 1;
-            const I8Host &H = dn ? D : U;
-            const size_t at = (size_t)((dn ? wv * (nkbd / 4) + 3 * j + cc : (12 * j + wv) * (nkbu / 4) + cc) * 32 * 4);
-            const size_t to = (size_t)((wv * ct + c) * 32 * 4);
-            std::memcpy(&S.d[to], &H.d[at], 32 * 4 * 4);
-            if (q1) std::memcpy(&S.m[to], &H.m[at], 32 * 4 * 4);
-            else std::memcpy(&S.dh[to], &H.dh[at], 32 * 4 * 2);
-        }
-    }
-    return upload_i8w(track, w, S);
-}
-
-// Repack a Q4_0 [N][K] matrix for the fp6-MFMA GEMMs (kernels.h F6W): per
-// (32-row f-tile, block) each row's 32 codes of q - 8 as e2m3 sign-magnitude
-// 6-bit fields at their Q8D positions (kernels_common.h q8d_pos), split into
-// a 16-byte and an 8-byte plane; the block scales as fp16 in the low half of
-// one dword per block (the d_w operand of the d_w * d_a MFMA).
-bool upload_f6(std::vector<void *> &track, F6W &w, const std::vector<const uint8_t *> &rows, int64_t K) {
-    const int64_t N = (int64_t)rows.size(), nkb = K / 32, nft = N / 32;
-    std::vector<uint32_t> q16((size_t)(N * nkb * 4)), q8((size_t)(N * nkb * 2)), dw((size_t)(N * nkb));
-    for (int64_t ft = 0; ft < nft; ft++)
-        for (int64_t b = 0; b < nkb; b++)
-            for (int m = 0; m < 32; m++) {
-                const uint8_t *blk = rows[(size_t)(32 * ft + m)] + b * 18;
-                uint32_t c6[6] = {0, 0, 0, 0, 0, 0};
-                for (int e = 0; e < 32; e++) {
-                    const uint8_t byte = blk[2 + (e & 15)];
-                    const int v = (e < 16 ? (byte & 15) : (byte >> 4)) - 8;
-                    const uint32_t code = (v < 0 ? 32u : 0u) | (uint32_t)(v < 0 ? -v : v);
-                    const int pos = 8 * (e >> 3) + 2 * (e & 3) + ((e >> 2) & 1);  // kernels_common.h q8d_pos
-                    const int bit = 6 * pos, wd = bit >> 5, o = bit & 31;
-                    c6[wd] |= code << o;
-                    if (o > 26) c6[wd + 1] |= code >> (32 - o);
-                }
-                const size_t i = (size_t)((ft * nkb + b) * 32 + m);
-                for (int k = 0; k < 4; k++) q16[i * 4 + k] = c6[k];
-                q8[i * 2] = c6[4];
-                q8[i * 2 + 1] = c6[5];
-                uint16_t dh;
-                std::memcpy(&dh, blk, 2);
-                dw[(size_t)((((ft * (nkb / 4) + b / 4) * 32) + m) * 4 + (b & 3))] = dh;
-            }
-    void *p16 = nullptr, *p8 = nullptr, *pd = nullptr;
-    if (!upload(track, &p16, q16.data(), q16.size() * 4) || !upload(track, &p8, q8.data(), q8.size() * 4) ||
-        !upload(track, &pd, dw.data(), dw.size() * 4))
-        return false;
-    w.q16 = (const uint4 *)p16;
-    w.q8 = (const uint2 *)p8;
-    w.dw = (const uint4 *)pd;
-    return true;
-}
-
 bool upload_packed(std::vector<void *> &track, WPtr &w, const Packed &p) {
     void *q = nullptr;
     if (!upload(track, &q, p.q.data(), p.q.size())) return false;
@@ -618,15 +475,10 @@ std::vector<const uint8_t *> rows_of(const GGUFTensor *t) {
     return r;
 }
 
-// The activation format of the O / FFN GEMM inputs (Ca, Ua, Xd; kernels.h
-// WType).  Xa, the LN output the QKV GEMMs read, is always ctx->wtype's.
-int act_type(const bert_ctx *ctx) { return ctx->f6 ? W_Q4_0D : ctx->wtype; }
-
-// activation format of a row of K values: element / block-scale bytes
-size_t act_row_bytes(int at, int64_t K) {
-    return at == W_Q4_0D ? (size_t)(K / 32) * Q8D_BLK : (size_t)K * (at == W_F32 ? 4 : at == W_F16 ? 2 : 1);
-}
-size_t act_scale_bytes(int at) { return at == W_Q4_0 || at == W_Q4_0D ? 2 : at == W_Q4_1 ? 4 : 0; }
+// activation format (ggml's vec_dot_type of the weights, kernels.h WType) of
+// a row of K values: element / block-scale bytes
+size_t act_row_bytes(int at, int64_t K) { return (size_t)K * (at == W_F32 ? 4 : at == W_F16 ? 2 : 1); }
+size_t act_scale_bytes(int at) { return at == W_Q4_0 ? 2 : at == W_Q4_1 ? 4 : 0; }
 
 // Activation buffers carry GEMM_BM spare rows: qkv_attention_kernel reads the
 // 128-row tile starting at each sentence's first token (rows past M are
@@ -662,11 +514,10 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
     w.cap_rows = w.cap_seqs = 0;
     w.X = w.out = nullptr;
     w.qk_hi = w.qk_lo = w.vt_hi = w.vt_lo = nullptr;
-    w.Xa = w.Ca = w.Ua = w.Xd = ActPtr{};
+    w.Xa = w.Ca = w.Ua = ActPtr{};
     w.tok = w.off = w.rowpos = w.tiles = w.perm = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
-    const int at = act_type(ctx);
-    if (ctx->f6 && !alloc_act(w.allocs, w.Xd, W_Q4_0D, rows, E, st)) return false;
+    const int at = ctx->wtype;
     if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
         !dmalloc(w.allocs, &w.qk_lo, (size_t)rows * 2 * E * 2) || !dmalloc(w.allocs, &w.vt_hi, (size_t)rows * E * 2) ||
         !dmalloc(w.allocs, &w.vt_lo, (size_t)rows * E * 2) ||
@@ -751,21 +602,18 @@ bool ws_release(Lane &ln, hipStream_t st) {
 // 1 B/weight, exact isum per block on the int8 MFMA, d_w * d_a applied in
 // the kernel like ggml's vec_dot).  Default: FFN-up (faster than the
 // split-fp16 GEMM) and FFN-down (as fast on full batches, faster on ragged
-// ones); the O projection stays on the split-fp16 GEMM.  Env
-// BERT_AMD_I8 (read at load): "0" none, "1" / "all" all three, or a comma list
-// of up, o, down.
-void i8_select(bert_ctx *ctx) {
-    const char *e = std::getenv("BERT_AMD_I8");
-    // default: FFN-up and FFN-down (tools/ab_bench.sh: down on int8 equals the split
-    // kernel on the full 1024 x 128 batch and is 3 % faster on ragged batches;
-    // o-proj on int8 is 20 % slower)
+// ones) where its LayerNorm is fused (n_embd 384); the O projection stays on
+// the split-fp16 GEMM.  `v` (load option "i8", env
+// BERT_AMD_I8): "0" none, "1" / "all" all three, or a list of up, o, down
+// separated by '+' or ','; empty: the default.
+void i8_select(bert_ctx *ctx, const std::string &spec) {
     // (the down GEMM only where its LayerNorm is fused, E = 384: wider rows use
     // the int8 residual kernel + launch_ln, 8 % slower than split-fp16 on C5)
-    const std::string v = e ? e : (ctx->hp.n_embd == 384 ? "up,down" : "up");
+    std::string v = spec.empty() ? (ctx->hp.n_embd == 384 ? "up,down" : "up") : spec;
+    std::replace(v.begin(), v.end(), '+', ',');
     const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const bool q4 = ctx->wtype == W_Q4_0 || ctx->wtype == W_Q4_1;
     const int ln = E == 384 ? EPI_LN : EPI_RESID;
-    // "0": none, "1" / "all": every projection, else a comma list of up, o, down
     const bool all = v == "1" || v == "all";
     auto has = [&](const char *p) {
         const std::string t = std::string(",") + v + ",";
@@ -776,47 +624,6 @@ void i8_select(bert_ctx *ctx) {
     ctx->i8_down = q4 && has("down") && i8_gemm_supported(ln, E, I);
 }
 
-// Q4_0 models of n_embd 384 (MiniLM) run the O, FFN-up and FFN-down GEMMs on
-// the fp6 MFMA (gemm_f6.hip: bitwise the int8 path's results, faster), their
-// activations stored as Q8D.  Opt-in for now (env BERT_AMD_F6=1, read at
-// load): in the full pipeline it does not yet beat the int8 kernels.
-void f6_select(bert_ctx *ctx) {
-    const char *e = std::getenv("BERT_AMD_F6");
-    const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
-    ctx->f6 = e && e[0] == '1' && ctx->wtype == W_Q4_0 && E == 384 && f6_gemm_supported(EPI_GELU_ACT, I, E) &&
-              f6_gemm_supported(EPI_LN, E, E) && f6_gemm_supported(EPI_LN, E, I);
-    if (ctx->f6) ctx->i8_o = ctx->i8_up = ctx->i8_down = false;
-}
-
-// The fused FFN kernel (gemm_i8.hip i8_ffn384_kernel) where the int8 FFN-up and
-// FFN-down + LN kernels run: n_embd 384, I % 384 == 0.  Opt-in (bitwise the
-// two-kernel path, 5 % slower on the headline batch): env
-// BERT_AMD_FFN=1 (read at load) or bert_amd_set_option "ffn_fused".
-void ffn_select(bert_ctx *ctx) {
-    const char *e = std::getenv("BERT_AMD_FFN");
-    ctx->ffn_ok = ctx->i8_up && ctx->i8_down && !ctx->f6 && i8_ffn_supported(ctx->hp.n_embd, ctx->hp.n_intermediate);
-    ctx->ffn_fused = ctx->ffn_ok && e && e[0] == '1';
-}
-
-// Q4 weights as nibbles with in-kernel dequant (kernels.h W_Q4_0N / W_Q4_1N):
-// env BERT_AMD_Q4NIB=1 (read at load).  Q4_0 (n_embd 384): the QKV (fused and
-// unfused) and O weights; not with the fp6 path, whose fused kernel stores a
-// Q8D context.  Q4_1: the unfused QKV and the split-path O and FFN-down
-// weights (the fused QKV + attention kernel keeps the split planes).
-void nib_select(bert_ctx *ctx) {
-    const char *e = std::getenv("BERT_AMD_Q4NIB");
-    const bool on = e && e[0] == '1';
-    ctx->q4nib = on && ((ctx->wtype == W_Q4_0 && !ctx->f6 && ctx->hp.n_embd == 384) || ctx->wtype == W_Q4_1);
-}
-// the weight type the unfused QKV / split O / split down launches name
-int qo_wtype(const bert_ctx *ctx) {
-    return !ctx->q4nib ? ctx->wtype : ctx->wtype == W_Q4_0 ? W_Q4_0N : W_Q4_1N;
-}
-// the split-path FFN-down weight type
-int down_wtype(const bert_ctx *ctx) { return ctx->q4nib && ctx->wtype == W_Q4_1 ? W_Q4_1N : ctx->wtype; }
-// the fused QKV + attention kernel's weight type
-int qkv_fused_wtype(const bert_ctx *ctx) { return ctx->f6 ? W_Q4_0D : ctx->wtype == W_Q4_0 ? qo_wtype(ctx) : ctx->wtype; }
-
 // One encoder layer over the row group [row0, row0 + rows) (sentences
 // d_off[0 .. nseq), absolute row offsets).  Xa / Ca / Ua / X point at the
 // group's first row; the QKV + attention kernels index rows absolutely through
@@ -824,7 +631,7 @@ int qkv_fused_wtype(const bert_ctx *ctx) { return ctx->f6 ? W_Q4_0D : ctx->wtype
 // with one group, row0 == 0).
 bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
                const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
-               ActPtr Ca, ActPtr Ua, ActPtr Xd, float *X, hipStream_t st) {
+               ActPtr Ca, ActPtr Ua, float *X, hipStream_t st) {
     const HParams &hp = ctx->hp;
     Workspace &w = ln.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
@@ -862,48 +669,11 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(qkv_fused_wtype(ctx), qf, aa, ntiles, st));
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
         } else {
-            LAUNCH_OK("gemm_qkv", launch_gemm(qo_wtype(ctx), EPI_QKV, 0, q, (int)rows, st));
-            LAUNCH_OK("attention", launch_attention(act_type(ctx), D, aa, nseq, max_len, st));
+            LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
+            LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
         }
-        if (ctx->f6) {  // O + LN, FFN up + GELU, FFN down + LN on the fp6 MFMA, Q8D in
-            GemmArgs o;
-            o.A = Ca;
-            o.K = E;
-            o.N = E;
-            o.Wf = L.o6;
-            o.bias = L.b_o;
-            o.X = X;
-            o.out_act = Xd;
-            o.ln_w = L.ln1_w;
-            o.ln_b = L.ln1_b;
-            o.eps = hp.eps;
-            LAUNCH_OK("gemm_o_ln", launch_gemm_f6(EPI_LN, o, (int)rows, st, W_Q4_0D));
-            GemmArgs u;
-            u.A = Xd;
-            u.K = E;
-            u.N = I;
-            u.Wf = L.up6;
-            u.bias = L.b_up;
-            u.out_act = Ua;
-            u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
-            LAUNCH_OK("gemm_up_gelu", launch_gemm_f6(EPI_GELU_ACT, u, (int)rows, st, W_Q4_0D));
-            GemmArgs dn;
-            dn.A = Ua;
-            dn.K = I;
-            dn.N = E;
-            dn.Wf = L.down6;
-            dn.bias = L.b_down;
-            dn.X = X;
-            dn.out_act = Xa;
-            dn.ln_w = L.ln2_w;
-            dn.ln_b = L.ln2_b;
-            dn.eps = hp.eps;
-            LAUNCH_OK("gemm_down_ln", launch_gemm_f6(EPI_LN, dn, (int)rows, st, W_Q4_0));  // next layer's QKV input
-            return true;
-        }
-
         GemmArgs o;
         o.A = Ca;
         o.K = E;
@@ -924,11 +694,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
-            LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_LN, 0, o, (int)rows, st));
-        } else if (ctx->resln) {
-            LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_RESLN, 0, o, (int)rows, st));
+            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)rows, st));
         } else {
-            LAUNCH_OK("gemm_o_ln", launch_gemm(qo_wtype(ctx), EPI_RESID, 0, o, (int)rows, st));
+            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
         }
 
@@ -953,11 +721,6 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         dn.ln_w = L.ln2_w;
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
-        if (ctx->ffn_fused) {  // U stays in the workgroup: Ua is not touched
-            u.Wi = L.ffn8;
-            LAUNCH_OK("gemm_ffn_ln", launch_ffn_i8(wt, u, dn, (int)rows, st));
-            return true;
-        }
         if (ctx->i8_up) {
             u.Wi = L.up8;
             LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt, EPI_GELU_ACT, u, (int)rows, st));
@@ -974,11 +737,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
-            LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_LN, 0, dn, (int)rows, st));
-        } else if (ctx->resln) {
-            LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_RESLN, 0, dn, (int)rows, st));
+            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)rows, st));
         } else {
-            LAUNCH_OK("gemm_down_ln", launch_gemm(down_wtype(ctx), EPI_RESID, 0, dn, (int)rows, st));
+            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
         }
     }
@@ -1010,10 +771,19 @@ EmbedArgs embed_args(const bert_ctx *ctx, Replica &R, const Workspace &w, const 
     return ea;
 }
 
+// Test tap (bert_amd_debug_layers): device buffers receiving the residual
+// stream X and its Q8 / fp16 activation form Xa after every stage (stage 0 =
+// embeddings + LN, stage l + 1 = encoder layer l), M rows each.
+struct DebugTap {
+    float *X = nullptr;
+    char *q = nullptr, *d = nullptr;
+};
+
 // The fixed pipeline over a ragged batch already resident on the device.
 // d_out_row (optional): output row of each sentence of the batch.
 bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, const int32_t *d_off, const int32_t *h_off,
-                  int n_seqs, float *d_out, hipStream_t st, const int32_t *d_out_row = nullptr) {
+                  int n_seqs, float *d_out, hipStream_t st, const int32_t *d_out_row = nullptr,
+                  const DebugTap *tap = nullptr) {
     const HParams &hp = ctx->hp;
     const int64_t M = h_off[n_seqs];
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
@@ -1024,12 +794,21 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, wt = ctx->wtype;
     const bool ln_fused = gemm_ln_fused(wt, E);
     // QKV + attention in one kernel when every sentence fits one 128-row tile
-    // (env BERT_AMD_UNFUSED=1 forces the two-kernel path, for A/B checks)
-    static const bool force_unfused = std::getenv("BERT_AMD_UNFUSED") != nullptr;
-    const bool fused_qkv_attn = !force_unfused && n_seqs >= ctx->fuse_min && qkv_attention_supported(wt, E, H, max_len);
+    // (option "unfused" forces the two-kernel path, for A/B checks)
+    const bool fused_qkv_attn =
+        !ctx->unfused && n_seqs >= ctx->fuse_min && qkv_attention_supported(wt, E, H, max_len, ctx->qkva_ntw);
 
     const EmbedArgs ea = embed_args(ctx, R, w, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(ctx->wtype, ea, (int)Mpad, st));
+    auto tap_stage = [&](int stage) {
+        if (!tap) return true;
+        const size_t xb = (size_t)M * E * 4, qb = (size_t)M * act_row_bytes(wt, E), db = (size_t)M * (E / 32) * act_scale_bytes(wt);
+        HIP_OK(hipMemcpyAsync(tap->X + (size_t)stage * M * E, w.X, xb, hipMemcpyDeviceToDevice, st));
+        HIP_OK(hipMemcpyAsync(tap->q + (size_t)stage * qb, w.Xa.q, qb, hipMemcpyDeviceToDevice, st));
+        if (db) HIP_OK(hipMemcpyAsync(tap->d + (size_t)stage * db, w.Xa.d, db, hipMemcpyDeviceToDevice, st));
+        return true;
+    };
+    if (!tap_stage(0)) return false;
 
     // Row groups (default; ctx->split = 0 turns them off):
     // with the fused QKV + attention path the batch is split at a 128-row-aligned
@@ -1050,7 +829,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
     };
     Group G[2] = {{0, Mpad, 0, n_seqs, st}, {0, 0, 0, 0, nullptr}};
     int ng = 1;
-    if (ctx->split && fused_qkv_attn && ln_fused && n_seqs >= 512 && ln.stream2) {
+    if (ctx->split && !tap && fused_qkv_attn && ln_fused && n_seqs >= 512 && ln.stream2) {
         int best = -1;
         for (int s = 1; s < n_seqs; s++)
             if (h_off[s] % GEMM_BM == 0 &&
@@ -1107,17 +886,16 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
         if (a.d) a.d = (char *)a.d + row0 * (K / 32) * (int64_t)act_scale_bytes(at);
         return a;
     };
-    const int at = act_type(ctx);
-
-    for (int il = 0; il < hp.n_layer; il++)
+    for (int il = 0; il < hp.n_layer; il++) {
         for (int gi = 0; gi < ng; gi++) {
             const Group &gr = G[gi];
             if (!run_layer(ctx, R, ln, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, w.tiles + 2 * gr.seq0, ntl[gi],
                            max_len, fused_qkv_attn, ln_fused, act_rows(w.Xa, wt, gr.row0, E),
-                           act_rows(w.Ca, at, gr.row0, E), act_rows(w.Ua, at, gr.row0, I),
-                           act_rows(w.Xd, W_Q4_0D, gr.row0, E), w.X + gr.row0 * E, gr.s))
+                           act_rows(w.Ca, wt, gr.row0, E), act_rows(w.Ua, wt, gr.row0, I), w.X + gr.row0 * E, gr.s))
                 return false;
         }
+        if (!tap_stage(il + 1)) return false;
+    }
     if (ng == 2) {
         HIP_OK(hipEventRecord(ln.ev_join, ln.stream2));
         HIP_OK(hipStreamWaitEvent(st, ln.ev_join, 0));
@@ -1245,14 +1023,14 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                     const GGUFTensor *bt = part == 0 ? l.q_b : part == 1 ? l.k_b : l.v_b;
                     bqkv[dst] = ((const float *)bt->data)[src];
                 }
-        if (qkv_attention_supported(ctx->wtype, (int)E, (int)ctx->hp.n_head, 128)) {
+        if (qkv_attention_supported(ctx->wtype, (int)E, (int)ctx->hp.n_head, 128, ctx->qkva_ntw)) {
             // undo repack's column interleave (row 32p + 2c + t <- 32p + 16t + c) so
             // that repacked tile j holds features 16j .. 16j + 15 in order
             // after the grouped tile order (kernels.hip qkv_attention_kernel): tile
             // G tpp q + G w + t <- n-tile w of 192-feature unit G q + t (tpp = 12
             // n-tiles per unit: a head pair at head dim 32, one head at 64; G =
             // units per main loop; G = 1 is the plain order)
-            const size_t tpp = 12, G = (size_t)qkv_attention_ntw(ctx->wtype);
+            const size_t tpp = 12, G = (size_t)ctx->qkva_ntw;
             std::vector<const uint8_t *> quad(rows.size()), plain(rows.size());
             for (size_t T = 0; T < rows.size() / 16; T++) {
                 const size_t src = tpp * (G * (T / (G * tpp)) + T % G) + (T % (G * tpp)) / G;
@@ -1261,7 +1039,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
             for (size_t pr = 0; pr < rows.size() / 32; pr++)
                 for (int t = 0; t < 2; t++)
                     for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = quad[32 * pr + 16 * t + c];
-            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E, ctx->q4nib && wt == GT_Q4_0))) return false;
+            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E))) return false;
         }
         std::vector<const uint8_t *> up_rows = rows_of(l.i_w);
         if (gemm_gelu_blk8(ctx->wtype)) {
@@ -1273,19 +1051,13 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                 for (int t = 0; t < 2; t++)
                     for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
         }
-        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E, ctx->q4nib))) return false;
-        // each projection in the one format its GEMM reads (fp6, int8 or split fp16)
-        if (ctx->f6) {
-            if (!upload_f6(tr, dl.o6, rows_of(l.o_w), E) || !upload_f6(tr, dl.up6, rows_of(l.i_w), E) ||
-                !upload_f6(tr, dl.down6, rows_of(l.o2_w), I))
-                return false;
-        } else if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E)
-                               : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E, ctx->q4nib))) ||
+        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
+        // each projection in the one format its GEMM reads (int8 or split fp16)
+        if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E))) ||
             !(ctx->i8_up ? upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) : upload_packed(tr, dl.up, repack(wt, up_rows, E))) ||
             !(ctx->i8_down ? upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I)
-                           : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I, down_wtype(ctx) == W_Q4_1N))))
+                           : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))))
             return false;
-        if (ctx->ffn_ok && !upload_ffn_i8(tr, dl.ffn8, wt, rows_of(l.i_w), rows_of(l.o2_w), E, I)) return false;
         if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
             !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||
             !upload(tr, &dl.ln1_w, l.ln1_w->data, E * 4) || !upload(tr, &dl.ln1_b, l.ln1_b->data, E * 4) ||
@@ -1336,7 +1108,85 @@ std::vector<int> parse_device_env(int n_visible) {
     return devs;
 }
 
-bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices) {
+// Context options (bert_amd.h bert_amd_set_option), checked; the caller
+// holds ctx->mu or owns the context.  Returns 0, or -2 with the error set.
+int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
+    auto need = [&](bool ok, const char *what) {
+        if (!ok) set_err("bert_amd option %s: %s", k.c_str(), what);
+        return ok ? 0 : -2;
+    };
+    if (k == "split") {
+        ctx->split = value != 0;
+    } else if (k == "pack") {
+        if (need(value >= -1 && value <= 1, "must be -1, 0 or 1")) return -2;
+        ctx->pack = value;
+    } else if (k == "fuse_min") {
+        if (need(value >= 0, "must be >= 0")) return -2;
+        ctx->fuse_min = value;
+    } else if (k == "unfused") {
+        ctx->unfused = value != 0;
+    } else if (k == "encode_lanes" || k == "encode_merge" || k == "encode_merge_rows") {
+        if (need(value >= 1, "must be >= 1")) return -2;
+        (k == "encode_lanes" ? ctx->encode_lanes : k == "encode_merge" ? ctx->encode_merge : ctx->encode_merge_rows) = value;
+    } else {
+        set_err("bert_amd option: unknown option '%s'", k.c_str());
+        return -2;
+    }
+    return 0;
+}
+
+// Load options (bert_amd.h bert_amd_load_opts): "key=value" items separated by
+// ';'.  Defaults come from the environment (BERT_AMD_<KEY>, upper case), read
+// here once per load and never again; the explicit string overrides them.
+// Load-time keys: i8 (the int8-MFMA projections, i8_select) and qkva_ntw (the
+// fused kernel's weight grouping); every bert_amd_set_option key is accepted
+// too.  Returns false with the error set.
+bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
+    static const char *keys[] = {"i8", "qkva_ntw", "split", "pack", "fuse_min", "unfused",
+                                 "encode_lanes", "encode_merge", "encode_merge_rows"};
+    std::vector<std::pair<std::string, std::string>> kv;
+    for (const char *k : keys) {
+        std::string env = "BERT_AMD_" + std::string(k);
+        for (char &c : env) c = (char)std::toupper((unsigned char)c);
+        if (const char *e = std::getenv(env.c_str()); e && *e) kv.push_back({k, e});
+    }
+    for (std::string o = opts ? opts : ""; !o.empty();) {
+        const size_t semi = o.find(';');
+        const std::string item = o.substr(0, semi);
+        o = semi == std::string::npos ? "" : o.substr(semi + 1);
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos || eq == 0) {
+            set_err("bert_amd_load_opts: malformed option '%s' (key=value expected)", item.c_str());
+            return false;
+        }
+        kv.push_back({item.substr(0, eq), item.substr(eq + 1)});
+    }
+    for (const auto &p : kv) {
+        if (p.first == "i8") {
+            i8_spec = p.second;
+            continue;
+        }
+        char *end = nullptr;
+        const long v = std::strtol(p.second.c_str(), &end, 10);
+        if (p.second.empty() || *end) {
+            set_err("bert_amd option %s: '%s' is not an integer", p.first.c_str(), p.second.c_str());
+            return false;
+        }
+        if (p.first == "qkva_ntw") {
+            if (v != 1 && v != 2) {
+                set_err("bert_amd option qkva_ntw: must be 1 or 2");
+                return false;
+            }
+            ctx->qkva_ntw = (int)v;
+        } else if (apply_option(ctx, p.first, (int32_t)v) != 0) {
+            return false;
+        }
+    }
+    return true;
+}
+
+bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices, const char *opts) {
     if (!fname) {
         set_err("null model path");
         return nullptr;
@@ -1455,17 +1305,9 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
                 tables().gelu_pair.size(), tables().exp_c.compact.size());
         return nullptr;
     }
-    i8_select(ctx.get());
-    f6_select(ctx.get());
-    nib_select(ctx.get());
-    ffn_select(ctx.get());
-    if (const char *e = std::getenv("BERT_AMD_SPLIT")) ctx->split = e[0] != '0';
-    if (const char *e = std::getenv("BERT_AMD_PACK")) ctx->pack = e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
-    if (const char *e = std::getenv("BERT_AMD_FUSE_MIN")) ctx->fuse_min = std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("BERT_AMD_ENCODE_LANES")) ctx->encode_lanes = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("BERT_AMD_ENCODE_MERGE")) ctx->encode_merge = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("BERT_AMD_RESLN")) ctx->resln = e[0] == '1';
-    if (const char *e = std::getenv("BERT_AMD_ENCODE_MERGE_ROWS")) ctx->encode_merge_rows = std::max(1, std::atoi(e));
+    std::string i8_spec;
+    if (!parse_load_options(ctx.get(), opts, i8_spec)) return nullptr;
+    i8_select(ctx.get(), i8_spec);
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {
@@ -1622,7 +1464,7 @@ int greedy_tiles(const int32_t *ntok, const std::vector<int> &order) {
 template <typename F>
 void eval_grouped(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs, F run) {
     const HParams &hp = ctx->hp;
-    if (!qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, GEMM_BM)) {
+    if (!qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, GEMM_BM, ctx->qkva_ntw)) {
         run(n, toks, ntok, embs);
         return;
     }
@@ -1661,31 +1503,51 @@ void encode_slices(bert_ctx *ctx, int32_t n, int32_t chunk, bert_vocab_id **toks
     const int nl = std::max(1, std::min(ctx->encode_lanes, (nslice + nr - 1) / nr));
     for (auto &r : ctx->reps) {
         if ((int)r->lanes.size() >= nl) continue;
-        if (hipSetDevice(r->device) != hipSuccess) return;
+        if (hipSetDevice(r->device) != hipSuccess) {
+            set_err("bert_encode_batch: hipSetDevice(%d) failed", r->device);
+            std::fprintf(stderr, "%s\n", g_err.c_str());
+            return;
+        }
         while ((int)r->lanes.size() < nl)
             if (!add_lane(*r)) {
-                std::fprintf(stderr, "bert_encode_batch: %s\n", g_err.c_str());
+                set_err("bert_encode_batch: lane creation failed: %s", g_err.c_str());
+                std::fprintf(stderr, "%s\n", g_err.c_str());
                 return;
             }
     }
+    // every worker's failures are collected (g_err is per thread) and reported
+    // on the calling thread; nothing escapes a worker (an exception leaving a
+    // std::thread would terminate the process)
     std::atomic<int> next{0};
     std::vector<std::thread> th;
+    std::vector<std::string> errs((size_t)nr * nl);
     for (int r = 0; r < nr; r++)
         for (int l = 0; l < nl; l++)
             th.emplace_back([&, r, l] {
-                Replica &R = *ctx->reps[r];
-                Lane &ln = *R.lanes[l];
-                for (int k = next++; k < nslice; k = next++) {
-                    const int32_t s0 = k * chunk, m = std::min(chunk, n - s0);
-                    eval_grouped(ctx, m, toks + s0, ntok + s0, embs + s0,
-                                 [&](int32_t mm, bert_vocab_id **t, int32_t *c, float **e) {
-                                     if (!eval_host_slice(ctx, R, ln, t, c, e, 0, mm))
-                                         std::fprintf(stderr, "bert_encode_batch: device %d: %s\n", R.device,
-                                                      g_err.c_str());
-                                 });
+                std::string &err = errs[(size_t)r * nl + l];
+                try {
+                    Replica &R = *ctx->reps[r];
+                    Lane &ln = *R.lanes[l];
+                    for (int k = next++; k < nslice; k = next++) {
+                        const int32_t s0 = k * chunk, m = std::min(chunk, n - s0);
+                        eval_grouped(ctx, m, toks + s0, ntok + s0, embs + s0,
+                                     [&](int32_t mm, bert_vocab_id **t, int32_t *c, float **e) {
+                                         if (!eval_host_slice(ctx, R, ln, t, c, e, 0, mm) && err.empty())
+                                             err = "device " + std::to_string(R.device) + ": " + g_err;
+                                     });
+                    }
+                } catch (const std::exception &e) {
+                    if (err.empty()) err = e.what();
+                } catch (...) {
+                    if (err.empty()) err = "unknown exception";
                 }
             });
     for (auto &t : th) t.join();
+    for (const std::string &e : errs)
+        if (!e.empty()) {
+            std::fprintf(stderr, "bert_encode_batch: %s\n", e.c_str());
+            set_err("bert_encode_batch: %s", e.c_str());
+        }
 }
 
 // Host-pointer batch eval, sharded over the context's replicas by token count.
@@ -1738,12 +1600,21 @@ void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *nto
     std::vector<std::string> errs(nr);
     for (int r = 0; r < nr; r++)
         th.emplace_back([&, r] {
-            if (!eval_host_slice(ctx, *ctx->reps[r], *ctx->reps[r]->lanes[0], toks, ntok, embs, cut[r], cut[r + 1]))
-                errs[r] = g_err;
+            try {
+                if (!eval_host_slice(ctx, *ctx->reps[r], *ctx->reps[r]->lanes[0], toks, ntok, embs, cut[r], cut[r + 1]))
+                    errs[r] = g_err;
+            } catch (const std::exception &e) {
+                errs[r] = e.what();
+            } catch (...) {
+                errs[r] = "unknown exception";
+            }
         });
     for (auto &t : th) t.join();
     for (int r = 0; r < nr; r++)
-        if (!errs[r].empty()) std::fprintf(stderr, "bert_eval_batch: device %d: %s\n", ctx->reps[r]->device, errs[r].c_str());
+        if (!errs[r].empty()) {
+            std::fprintf(stderr, "bert_eval_batch: device %d: %s\n", ctx->reps[r]->device, errs[r].c_str());
+            set_err("bert_eval_batch: device %d: %s", ctx->reps[r]->device, errs[r].c_str());
+        }
 }
 
 }  // namespace
@@ -1780,7 +1651,7 @@ bool bert_params_parse(int argc, char **argv, bert_params &params) {
 bert_ctx *bert_load_from_file(const char *fname) {
     bert_ctx *c = nullptr;
     try {
-        c = load_impl(fname, nullptr, 0);
+        c = load_impl(fname, nullptr, 0, nullptr);
     } catch (const std::exception &e) {
         set_err("%s", e.what());
         c = nullptr;
@@ -1916,8 +1787,12 @@ const char *bert_vocab_id_to_token(bert_ctx *ctx, bert_vocab_id id) {
 // ============================================================ extensions (bert_amd.h)
 
 bert_ctx *bert_amd_load(const char *fname, const int32_t *devices, int32_t n_devices) {
+    return bert_amd_load_opts(fname, devices, n_devices, nullptr);
+}
+
+bert_ctx *bert_amd_load_opts(const char *fname, const int32_t *devices, int32_t n_devices, const char *options) {
     try {
-        return load_impl(fname, devices, n_devices);
+        return load_impl(fname, devices, n_devices, options);
     } catch (const std::exception &e) {
         set_err("%s", e.what());
         return nullptr;
@@ -1973,7 +1848,7 @@ int32_t bert_amd_eval_device(bert_ctx *ctx, int32_t slot, const int32_t *d_token
         std::vector<int32_t> ntok(n_seqs);
         int max_len = 0;
         for (int s = 0; s < n_seqs; s++) max_len = std::max(max_len, ntok[s] = h_offsets[s + 1] - h_offsets[s]);
-        if (n_seqs > 1 && qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, max_len)) {
+        if (n_seqs > 1 && qkv_attention_supported(ctx->wtype, hp.n_embd, hp.n_head, max_len, ctx->qkva_ntw)) {
             std::vector<int> idx(n_seqs);
             for (int s = 0; s < n_seqs; s++) idx[s] = s;
             const std::vector<int> order = tile_order(ntok.data(), idx);
@@ -2092,58 +1967,70 @@ int32_t bert_amd_debug_embed(bert_ctx *ctx, const int32_t *tokens, const int32_t
     return 0;
 }
 
+int32_t bert_amd_debug_layers(bert_ctx *ctx, const int32_t *tokens, const int32_t *offsets, int32_t n_seqs,
+                              float *X_out, void *q_out, void *d_out) {
+    if (!ctx || !tokens || !offsets || n_seqs <= 0 || !X_out || !q_out) {
+        set_err("bert_amd_debug_layers: invalid arguments");
+        return -1;
+    }
+    const int64_t M = offsets[n_seqs];
+    for (int s = 0; s < n_seqs; s++)
+        if (offsets[s + 1] - offsets[s] <= 0 || offsets[s + 1] - offsets[s] > ctx->hp.n_max_tokens) {
+            set_err("bert_amd_debug_layers: bad sentence length");
+            return -2;
+        }
+    for (int64_t i = 0; i < M; i++)
+        if (tokens[i] < 0 || tokens[i] >= ctx->hp.n_vocab) {
+            set_err("bert_amd_debug_layers: token id out of range");
+            return -2;
+        }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Replica &R = *ctx->reps[0];
+    std::vector<void *> bufs;
+    struct Free {
+        std::vector<void *> &b;
+        ~Free() {
+            for (void *p : b) hipFree(p);
+        }
+    } fr{bufs};
+    try {
+        HIP_OK_RC(hipSetDevice(R.device), -3);
+        Lane &ln = *R.lanes[0];
+        const hipStream_t st = ln.stream;
+        const int64_t E = ctx->hp.n_embd, S = ctx->hp.n_layer + 1;
+        const size_t xb = (size_t)(M * E) * 4, qb = (size_t)M * act_row_bytes(ctx->wtype, E),
+                     db = (size_t)(M * (E / 32)) * act_scale_bytes(ctx->wtype);
+        DebugTap tap;
+        int32_t *d_tok = nullptr, *d_off = nullptr;
+        float *d_emb = nullptr;
+        if (!dmalloc(bufs, &tap.X, S * xb) || !dmalloc(bufs, &tap.q, S * qb) || !dmalloc(bufs, &tap.d, S * db + 16) ||
+            !dmalloc(bufs, &d_tok, (size_t)M * 4) || !dmalloc(bufs, &d_off, (size_t)(n_seqs + 1) * 4) ||
+            !dmalloc(bufs, &d_emb, (size_t)n_seqs * E * 4))
+            return -3;
+        HIP_OK_RC(hipMemcpy(d_tok, tokens, (size_t)M * 4, hipMemcpyHostToDevice), -3);
+        HIP_OK_RC(hipMemcpy(d_off, offsets, (size_t)(n_seqs + 1) * 4, hipMemcpyHostToDevice), -3);
+        if (!ws_acquire(ln, st)) return -3;
+        const bool ok = run_pipeline(ctx, R, ln, d_tok, d_off, offsets, n_seqs, d_emb, st, nullptr, &tap);
+        ws_release(ln, st);
+        HIP_OK_RC(hipStreamSynchronize(st), -3);
+        if (!ok) return -4;
+        HIP_OK_RC(hipMemcpy(X_out, tap.X, S * xb, hipMemcpyDeviceToHost), -3);
+        HIP_OK_RC(hipMemcpy(q_out, tap.q, S * qb, hipMemcpyDeviceToHost), -3);
+        if (d_out && db) HIP_OK_RC(hipMemcpy(d_out, tap.d, S * db, hipMemcpyDeviceToHost), -3);
+    } catch (const std::exception &e) {
+        set_err("%s", e.what());
+        return -5;
+    }
+    return 0;
+}
+
 int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
     if (!ctx || !key) {
         set_err("bert_amd_set_option: invalid arguments");
         return -1;
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
-    const std::string k = key;
-    if (k == "split") {
-        ctx->split = value != 0;
-    } else if (k == "pack") {
-        if (value < -1 || value > 1) {
-            set_err("bert_amd_set_option: pack must be -1, 0 or 1");
-            return -2;
-        }
-        ctx->pack = value;
-    } else if (k == "encode_merge") {
-        if (value < 1) {
-            set_err("bert_amd_set_option: encode_merge must be >= 1");
-            return -2;
-        }
-        ctx->encode_merge = value;
-    } else if (k == "resln") {
-        ctx->resln = value != 0;
-    } else if (k == "encode_merge_rows") {
-        if (value < 1) {
-            set_err("bert_amd_set_option: encode_merge_rows must be >= 1");
-            return -2;
-        }
-        ctx->encode_merge_rows = value;
-    } else if (k == "encode_lanes") {
-        if (value < 1) {
-            set_err("bert_amd_set_option: encode_lanes must be >= 1");
-            return -2;
-        }
-        ctx->encode_lanes = value;
-    } else if (k == "ffn_fused") {
-        if (value != 0 && !ctx->ffn_ok) {
-            set_err("bert_amd_set_option: ffn_fused needs an n_embd 384 Q4 model on the int8 FFN kernels");
-            return -2;
-        }
-        ctx->ffn_fused = value != 0;
-    } else if (k == "fuse_min") {
-        if (value < 0) {
-            set_err("bert_amd_set_option: fuse_min must be >= 0");
-            return -2;
-        }
-        ctx->fuse_min = value;
-    } else {
-        set_err("bert_amd_set_option: unknown option '%s'", key);
-        return -2;
-    }
-    return 0;
+    return apply_option(ctx, key, value);
 }
 
 int64_t bert_amd_workspace_rows(bert_ctx *ctx, int32_t slot) {

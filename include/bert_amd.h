@@ -29,6 +29,20 @@ extern "C" {
    env BERT_AMD_DEVICES="0,1,...".  Returns NULL on error. */
 BERT_API struct bert_ctx *bert_amd_load(const char *fname, const int32_t *devices, int32_t n_devices);
 
+/* bert_amd_load with options: "key=value" items separated by ';' (NULL or ""
+   = none).  Every key's default may come from the environment
+   (BERT_AMD_<KEY> in upper case), which is read once, inside this call; the
+   string overrides it.  Load-time keys (they shape the device weights):
+     "i8"       Q4 projections on the int8-MFMA GEMMs: "0" none, "all", or a
+                list of up, o, down joined by '+' (default: up+down at n_embd
+                384, up otherwise)
+     "qkva_ntw" 1 | 2   head-pair units per main loop of the fused QKV +
+                attention kernel (default 2)
+   and every bert_amd_set_option key below.  Returns NULL on error (an unknown
+   key or a bad value included). */
+BERT_API struct bert_ctx *bert_amd_load_opts(const char *fname, const int32_t *devices, int32_t n_devices,
+                                             const char *options);
+
 BERT_API int32_t bert_amd_n_devices(struct bert_ctx *ctx);
 
 /* hparams: [n_vocab, n_max_tokens, n_embd, n_intermediate, n_head, n_layer, weight ggml type] */
@@ -82,24 +96,31 @@ BERT_API int32_t bert_amd_tokenize_json(const char *tokenizer_json, const char *
 BERT_API int32_t bert_amd_debug_embed(struct bert_ctx *ctx, const int32_t *tokens, const int32_t *offsets,
                                       int32_t n_seqs, float *X_out, void *q_out, void *d_out);
 
+/* Test hook: the whole pipeline on a host batch (replica 0, one row group,
+   the kernels bert_eval_batch would pick for it under the context's options),
+   copying back the residual stream after every stage: X_out f32
+   [n_layer + 1][M][n_embd] (stage 0 = embeddings + LayerNorm, reference
+   bert.cpp:865-898; stage l + 1 = the output of encoder layer l,
+   bert.cpp:900-993) and its activation form as bert_amd_debug_embed's q / d,
+   per stage.  Lets tests pin parity layer by layer against the oracle. */
+BERT_API int32_t bert_amd_debug_layers(struct bert_ctx *ctx, const int32_t *tokens, const int32_t *offsets,
+                                       int32_t n_seqs, float *X_out, void *q_out, void *d_out);
+
 /* Rows (tokens, padded to the 128-row tile) the device workspace of replica
    `slot` currently holds; -1 on a bad argument.  Lets callers and tests see
    that bert_encode_batch's n_batch_size bounds the working set. */
 BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
 
-/* Per-context pipeline options (read from the environment once at load,
-   BERT_AMD_SPLIT / BERT_AMD_PACK / BERT_AMD_FUSE_MIN / BERT_AMD_ENCODE_LANES;
-   this call changes them
-   afterwards):
+/* Per-context pipeline options (defaults, then bert_amd_load_opts /
+   BERT_AMD_<KEY> at load; this call changes them afterwards):
      "split" 0 | 1     run large fused batches as two row groups on two streams
      "pack"  -1 | 0 | 1 pack short sentences into shared fused-kernel tiles
                         when it pays (-1, default) / never / always
      "fuse_min" n >= 0 batches of fewer than n sentences (default 48) run the
                         unfused QKV GEMM + attention pair instead of the fused
                         kernel (lower latency for small batches)
-     "resln" 0 | 1      Q4 models of n_embd 768 / 1024: LayerNorm inside the O and
-                        FFN-down residual GEMMs (1) instead of a separate pass
-                        (0, default: faster; BERT_AMD_RESLN)
+     "unfused" 0 | 1    1: every batch on the QKV GEMM + attention pair (A/B
+                        checks; default 0)
      "encode_lanes" n >= 1 bert_encode_batch: lanes per device, each a host
                         thread with its own workspace and streams (default 2;
                         BERT_AMD_ENCODE_LANES)

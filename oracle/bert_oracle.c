@@ -630,75 +630,74 @@ int oracle_embed_ln(void *vm, const int32_t *tokens, int N, float *x_out) {
     return 0;
 }
 
-int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
-    omodel *m = (omodel *)vm;
-    if (!m || N <= 0 || N > m->n_max) return -1;
+/* one encoder layer il on x[N][E] in place (bert.cpp:900-993) */
+static void encoder_layer(const omodel *m, int il, float *x, int N) {
     const int E = m->n_embd, I = m->n_inter, H = m->n_head, D = E / H;
-    for (int i = 0; i < N; i++) if (tokens[i] < 0 || tokens[i] >= m->word->ne[1]) return -2;
-    float *x = (float *)malloc((size_t)N * E * 4), *tmp = (float *)malloc((size_t)N * E * 4);
+    float *tmp = (float *)malloc((size_t)N * E * 4);
     float *qkv = (float *)malloc((size_t)3 * N * E * 4), *ctx = (float *)malloc((size_t)N * E * 4);
     float *u = (float *)malloc((size_t)N * I * 4), *x1 = (float *)malloc((size_t)N * E * 4);
-    embed_ln(m, tokens, N, x);
-
     const float kq_scale = 1.0f / sqrtf((float)D);
-    for (int il = 0; il < m->n_layer; il++) {
-        const struct olayer *L = &m->L[il];
-        act_t a = {0};
-        act_convert(&a, x, N, E, L->q_w->type);
-        float *Q = qkv, *K = qkv + (size_t)N * E, *V = qkv + (size_t)2 * N * E;
-        mul_mat_bias(L->q_w, L->q_b, &a, N, Q);
-        mul_mat_bias(L->k_w, L->k_b, &a, N, K);
-        mul_mat_bias(L->v_w, L->v_b, &a, N, V);
-        act_free(&a);
-        /* attention per head (bert.cpp:930-942) */
+    const struct olayer *L = &m->L[il];
+    act_t a = {0};
+    act_convert(&a, x, N, E, L->q_w->type);
+    float *Q = qkv, *K = qkv + (size_t)N * E, *V = qkv + (size_t)2 * N * E;
+    mul_mat_bias(L->q_w, L->q_b, &a, N, Q);
+    mul_mat_bias(L->k_w, L->k_b, &a, N, K);
+    mul_mat_bias(L->v_w, L->v_b, &a, N, V);
+    act_free(&a);
+    /* attention per head (bert.cpp:930-942) */
 #pragma omp parallel for schedule(static)
-        for (int h = 0; h < H; h++) {
-            float *kh = (float *)malloc((size_t)N * D * 4), *qh = (float *)malloc((size_t)N * D * 4);
-            float *vt = (float *)malloc((size_t)D * N * 4), *P = (float *)malloc((size_t)N * 4);
-            for (int t = 0; t < N; t++)
-                for (int j = 0; j < D; j++) {
-                    kh[t * D + j] = K[(size_t)t * E + h * D + j];
-                    qh[t * D + j] = Q[(size_t)t * E + h * D + j];
-                    vt[(size_t)j * N + t] = V[(size_t)t * E + h * D + j]; /* ggml_cont(transpose(V)) */
-                }
-            for (int q = 0; q < N; q++) {
-                float mx = -INFINITY;
-                for (int k = 0; k < N; k++) {
-                    P[k] = dot_f32(D, kh + k * D, qh + q * D) * kq_scale;  /* mul_mat(K,Q), scale */
-                    mx = P[k] > mx ? P[k] : mx;
-                }
-                double sum = 0.0;
-                for (int k = 0; k < N; k++) {
-                    if (P[k] == -INFINITY) { P[k] = 0.0f; continue; }
-                    const float val = F16(g_tab_exp[H16(P[k] - mx)]);
-                    sum += (double)val;
-                    P[k] = val;
-                }
-                const float r = (float)(1.0 / sum);
-                for (int k = 0; k < N; k++) P[k] *= r;
-                for (int j = 0; j < D; j++) ctx[(size_t)q * E + h * D + j] = dot_f32(N, vt + (size_t)j * N, P);
+    for (int h = 0; h < H; h++) {
+        float *kh = (float *)malloc((size_t)N * D * 4), *qh = (float *)malloc((size_t)N * D * 4);
+        float *vt = (float *)malloc((size_t)D * N * 4), *P = (float *)malloc((size_t)N * 4);
+        for (int t = 0; t < N; t++)
+            for (int j = 0; j < D; j++) {
+                kh[t * D + j] = K[(size_t)t * E + h * D + j];
+                qh[t * D + j] = Q[(size_t)t * E + h * D + j];
+                vt[(size_t)j * N + t] = V[(size_t)t * E + h * D + j]; /* ggml_cont(transpose(V)) */
             }
-            free(kh); free(qh); free(vt); free(P);
+        for (int q = 0; q < N; q++) {
+            float mx = -INFINITY;
+            for (int k = 0; k < N; k++) {
+                P[k] = dot_f32(D, kh + k * D, qh + q * D) * kq_scale;  /* mul_mat(K,Q), scale */
+                mx = P[k] > mx ? P[k] : mx;
+            }
+            double sum = 0.0;
+            for (int k = 0; k < N; k++) {
+                if (P[k] == -INFINITY) { P[k] = 0.0f; continue; }
+                const float val = F16(g_tab_exp[H16(P[k] - mx)]);
+                sum += (double)val;
+                P[k] = val;
+            }
+            const float r = (float)(1.0 / sum);
+            for (int k = 0; k < N; k++) P[k] *= r;
+            for (int j = 0; j < D; j++) ctx[(size_t)q * E + h * D + j] = dot_f32(N, vt + (size_t)j * N, P);
         }
-        /* O-proj + residual + LN (bert.cpp:945-962) */
-        act_convert(&a, ctx, N, E, L->o_w->type);
-        mul_mat_bias(L->o_w, L->o_b, &a, N, x1);
-        act_free(&a);
-        for (int64_t i = 0; i < (int64_t)N * E; i++) x1[i] = x1[i] + x[i];
-        layer_norm(x1, N, E, L->ln1_w, L->ln1_b, m->eps);
-        /* FFN (bert.cpp:967-992) */
-        act_convert(&a, x1, N, E, L->i_w->type);
-        mul_mat_bias(L->i_w, L->i_b, &a, N, u);
-        act_free(&a);
-#pragma omp parallel for schedule(static)
-        for (int64_t i = 0; i < (int64_t)N * I; i++) u[i] = F16(g_tab_gelu[H16(u[i])]);
-        act_convert(&a, u, N, I, L->o2_w->type);
-        mul_mat_bias(L->o2_w, L->o2_b, &a, N, tmp);
-        act_free(&a);
-        for (int64_t i = 0; i < (int64_t)N * E; i++) x[i] = x1[i] + tmp[i];
-        layer_norm(x, N, E, L->ln2_w, L->ln2_b, m->eps);
+        free(kh); free(qh); free(vt); free(P);
     }
-    /* mean pool as mul_mat(cont(transpose(x)), 1/N) then L2 (bert.cpp:995-1006) */
+    /* O-proj + residual + LN (bert.cpp:945-962) */
+    act_convert(&a, ctx, N, E, L->o_w->type);
+    mul_mat_bias(L->o_w, L->o_b, &a, N, x1);
+    act_free(&a);
+    for (int64_t i = 0; i < (int64_t)N * E; i++) x1[i] = x1[i] + x[i];
+    layer_norm(x1, N, E, L->ln1_w, L->ln1_b, m->eps);
+    /* FFN (bert.cpp:967-992) */
+    act_convert(&a, x1, N, E, L->i_w->type);
+    mul_mat_bias(L->i_w, L->i_b, &a, N, u);
+    act_free(&a);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)N * I; i++) u[i] = F16(g_tab_gelu[H16(u[i])]);
+    act_convert(&a, u, N, I, L->o2_w->type);
+    mul_mat_bias(L->o2_w, L->o2_b, &a, N, tmp);
+    act_free(&a);
+    for (int64_t i = 0; i < (int64_t)N * E; i++) x[i] = x1[i] + tmp[i];
+    layer_norm(x, N, E, L->ln2_w, L->ln2_b, m->eps);
+    free(tmp); free(qkv); free(ctx); free(u); free(x1);
+}
+
+/* mean pool as mul_mat(cont(transpose(x)), 1/N) then L2 (bert.cpp:995-1006) */
+static void pool_l2(const omodel *m, const float *x, int N, float *out) {
+    const int E = m->n_embd;
     float *col = (float *)malloc((size_t)N * 4), *inv = (float *)malloc((size_t)N * 4);
     const float invN = 1.0f / N;
     for (int t = 0; t < N; t++) inv[t] = invN;
@@ -712,7 +711,44 @@ int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
     const float r = 1.0f / len;
     for (int e = 0; e < E; e++) out[e] = out[e] * r;
     free(col); free(inv);
-    free(x); free(tmp); free(qkv); free(ctx); free(u); free(x1);
+}
+
+int oracle_eval(void *vm, const int32_t *tokens, int N, float *out) {
+    omodel *m = (omodel *)vm;
+    if (!m || N <= 0 || N > m->n_max) return -1;
+    for (int i = 0; i < N; i++) if (tokens[i] < 0 || tokens[i] >= m->word->ne[1]) return -2;
+    float *x = (float *)malloc((size_t)N * m->n_embd * 4);
+    embed_ln(m, tokens, N, x);
+    for (int il = 0; il < m->n_layer; il++) encoder_layer(m, il, x, N);
+    pool_l2(m, x, N, out);
+    free(x);
+    return 0;
+}
+
+/* Per-stage residual stream of one sentence (tests pin the GPU layer by
+   layer): xs_out[(n_layer + 1)][N][E], stage 0 the embedding LayerNorm
+   output, stage l + 1 the output of encoder layer l (bert.cpp:900-993). */
+int oracle_eval_layers(void *vm, const int32_t *tokens, int N, float *xs_out) {
+    omodel *m = (omodel *)vm;
+    if (!m || N <= 0 || N > m->n_max) return -1;
+    for (int i = 0; i < N; i++) if (tokens[i] < 0 || tokens[i] >= m->word->ne[1]) return -2;
+    const size_t st = (size_t)N * m->n_embd;
+    embed_ln(m, tokens, N, xs_out);
+    for (int il = 0; il < m->n_layer; il++) {
+        memcpy(xs_out + (il + 1) * st, xs_out + il * st, st * 4);
+        encoder_layer(m, il, xs_out + (il + 1) * st, N);
+    }
+    return 0;
+}
+
+/* One encoder layer il of one sentence from a given input x_in[N][E] (e.g.
+   the GPU's own previous-stage output): separates a layer's own error from
+   the error it inherits. */
+int oracle_layer(void *vm, int il, const float *x_in, int N, float *x_out) {
+    omodel *m = (omodel *)vm;
+    if (!m || N <= 0 || N > m->n_max || il < 0 || il >= m->n_layer) return -1;
+    memcpy(x_out, x_in, (size_t)N * m->n_embd * 4);
+    encoder_layer(m, il, x_out, N);
     return 0;
 }
 

@@ -57,6 +57,12 @@ def lib() -> ctypes.CDLL:
         L.oracle_embed_ln.restype = ctypes.c_int
         L.oracle_embed_ln.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_float)]
+        L.oracle_eval_layers.restype = ctypes.c_int
+        L.oracle_eval_layers.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_float)]
+        L.oracle_layer.restype = ctypes.c_int
+        L.oracle_layer.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_float)]
         _lib = L
     return _lib
 
@@ -93,6 +99,29 @@ class Oracle:
                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
         if rc != 0:
             raise RuntimeError(f"oracle_embed_ln failed ({rc})")
+        return out
+
+    def eval_layers(self, tokens) -> np.ndarray:
+        """The residual stream of one sentence after every stage: [n_layer + 1, N, E]
+        (stage 0 the embedding LayerNorm, stage l + 1 encoder layer l; reference
+        bert.cpp:865-993)."""
+        t = np.ascontiguousarray(np.asarray(tokens, np.int32))
+        out = np.zeros((self.n_layer + 1, len(t), self.n_embd), np.float32)
+        rc = self.L.oracle_eval_layers(self.m, t.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(t),
+                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        if rc != 0:
+            raise RuntimeError(f"oracle_eval_layers failed ({rc})")
+        return out
+
+    def layer(self, il: int, x: np.ndarray) -> np.ndarray:
+        """Encoder layer il (reference bert.cpp:900-993) of one sentence applied to a
+        given input stream x [N, E] (e.g. the GPU's own previous stage)."""
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.zeros_like(x)
+        rc = self.L.oracle_layer(self.m, il, x.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), x.shape[0],
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        if rc != 0:
+            raise RuntimeError(f"oracle_layer failed ({rc})")
         return out
 
     def eval_batch(self, token_lists, n_threads: int = 0) -> np.ndarray:

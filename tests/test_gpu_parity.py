@@ -112,148 +112,25 @@ def test_every_weight_type_vs_oracle(ftype, model_dir):
     assert c.min() >= COS_TOL, (ftype, 1 - c)
 
 
-@pytest.mark.parametrize("mode", ["1", "0"])
+@pytest.mark.parametrize("mode", ["all", "0"])
 @pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_1", "minilm_q4_0_std01"])
-def test_int8_gemm_path_golden(case, mode, model_dir, monkeypatch):
-    """Every Q4 projection on the int8-MFMA GEMMs (env BERT_AMD_I8=1:
+def test_int8_gemm_path_golden(case, mode, model_dir):
+    """Every Q4 projection on the int8-MFMA GEMMs (load option i8=all:
     gemm_i8.hip, scales applied in-kernel per block like
-    ggml_vec_dot_q4_x_q8_x), and every one on the split-fp16 GEMMs
-    (BERT_AMD_I8=0), against the same golden fixtures, bitwise deterministic
-    (the default mixes the two: up and down int8, o split-fp16)."""
+    ggml_vec_dot_q4_x_q8_x), and every one on the split-fp16 GEMMs (i8=0),
+    against the same golden fixtures, bitwise deterministic (the default
+    mixes the two: up and down int8, o split-fp16)."""
     meta, toks, want = load_case(case)
     p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    monkeypatch.setenv("BERT_AMD_I8", mode)
-    m = bertlib.BertModel(p)
+    m = bertlib.BertModel(p, options={"i8": mode})
     try:
         got = m.eval_batch(toks)
         assert np.array_equal(got, m.eval_batch(toks))
     finally:
         m.close()
     c = cos(got, want)
-    print(f"BERT_AMD_I8={mode} {case}: 1-cos max {1 - c.min():.2e}")
+    print(f"i8={mode} {case}: 1-cos max {1 - c.min():.2e}")
     assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
-
-
-@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01"])
-def test_q4_nibble_qkv_o_golden(case, model_dir, monkeypatch):
-    """QKV (fused and unfused) and O-projection weights as ggml nibbles,
-    dequantised inside the fp16 MFMA GEMM (env BERT_AMD_Q4NIB=1, kernels.h
-    W_Q4_0N: one MFMA gives the block's exact isum, the fold applies
-    d_w * d_a per block like ggml_vec_dot_q4_0_q8_0): golden fixtures within
-    the bound, deterministic, and the fused kernel bitwise the unfused pair."""
-    meta, toks, want = load_case(case)
-    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    monkeypatch.setenv("BERT_AMD_Q4NIB", "1")
-    m = bertlib.BertModel(p)
-    try:
-        got = m.eval_batch(toks)
-        assert np.array_equal(got, m.eval_batch(toks))
-        short = [t for t in toks if len(t) <= 128] * 8  # >= fuse_min: the fused kernel
-        m.set_option("fuse_min", 0)
-        fused = m.eval_batch(short)
-        m.set_option("fuse_min", 10 ** 6)
-        assert np.array_equal(m.eval_batch(short), fused)
-    finally:
-        m.close()
-    c = cos(got, want)
-    print(f"BERT_AMD_Q4NIB=1 {case}: 1-cos max {1 - c.min():.2e}")
-    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
-
-
-@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01", "minilm_q4_1"])
-def test_fused_ffn_bitwise_split(case, model_dir):
-    """FFN-up + GELU + FFN-down + LN in one kernel (gemm_i8.hip
-    i8_ffn384_kernel, the intermediate kept in LDS slice by slice): bitwise the
-    two-kernel int8 path (same block sums, GELU table, Q8 quantiser and
-    block order), and the golden fixtures within the bound."""
-    meta, toks, want = load_case(case)
-    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    m = bertlib.BertModel(p)
-    try:
-        m.set_option("ffn_fused", 1)
-        fused = m.eval_batch(toks)
-        assert np.array_equal(fused, m.eval_batch(toks))
-        m.set_option("ffn_fused", 0)
-        split = m.eval_batch(toks)
-    finally:
-        m.close()
-    assert np.array_equal(fused, split), np.abs(fused - split).max()
-    c = cos(fused, want)
-    print(f"fused FFN {case}: 1-cos max {1 - c.min():.2e}")
-    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
-
-
-@pytest.mark.parametrize("case", ["c5_bge_q4_1_l2", "c5_bge_q4_1_l2_short"])
-@pytest.mark.parametrize("nib", ["0", "1"])
-def test_residual_ln_fused_bitwise(case, nib, model_dir, monkeypatch):
-    """n_embd 1024 Q4 (C5, bge-large Q4_1): the O and FFN-down residual GEMMs
-    normalise their rows in the same kernel (kernels.hip EPI_RESLN: one
-    workgroup walks a row tile's column tiles, then ln_rows16 on its own rows)
-    — bitwise the EPI_RESID + launch_ln pair (reference bert.cpp:955-961,
-    985-991), on the split-plane and the nibble (BERT_AMD_Q4NIB=1) weights, on
-    the fused (short) and unfused (512-token) QKV paths; golden within the bound."""
-    meta, toks, want = load_case(case)
-    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    monkeypatch.setenv("BERT_AMD_Q4NIB", nib)
-    m = bertlib.BertModel(p)
-    try:
-        m.set_option("resln", 1)
-        fused = m.eval_batch(toks)
-        assert np.array_equal(fused, m.eval_batch(toks))
-        m.set_option("resln", 0)
-        pair = m.eval_batch(toks)
-    finally:
-        m.close()
-    assert np.array_equal(fused, pair), np.abs(fused - pair).max()
-    c = cos(fused, want)
-    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
-
-
-@pytest.mark.parametrize("case", ["c5_bge_q4_1_l2", "c5_bge_q4_1_l2_short", "minilm_q4_1"])
-def test_q4_1_nibble_golden(case, model_dir, monkeypatch):
-    """Q4_1 unfused-QKV, split O and FFN-down weights as ggml nibbles (env
-    BERT_AMD_Q4NIB=1, kernels.h W_Q4_1N: one MFMA gives the block's exact
-    isum of q_w * q_a, the fold adds d_w d_a isum + m_w s_a per block like
-    ggml_vec_dot_q4_1_q8_1): golden fixtures within the bound, deterministic,
-    small batches (unfused path) bitwise the same rows in a full batch."""
-    meta, toks, want = load_case(case)
-    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    monkeypatch.setenv("BERT_AMD_Q4NIB", "1")
-    m = bertlib.BertModel(p)
-    try:
-        m.set_option("fuse_min", 10 ** 6)  # every batch on the unfused QKV GEMM (nibbles)
-        got = m.eval_batch(toks)
-        assert np.array_equal(got, m.eval_batch(toks))
-        assert np.array_equal(m.eval_batch(toks[:3]), got[:3])
-    finally:
-        m.close()
-    c = cos(got, want)
-    print(f"BERT_AMD_Q4NIB=1 {case}: 1-cos max {1 - c.min():.2e}")
-    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
-
-
-@pytest.mark.parametrize("case", ["c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01"])
-def test_fp6_gemm_path_bitwise_int8(case, model_dir, monkeypatch):
-    """O / FFN-up / FFN-down on the fp6-MFMA GEMMs (env BERT_AMD_F6=1:
-    gemm_f6.hip, Q8D activations, isum as two exact fp6 digit-plane MFMAs,
-    the same per-block fold as gemm_i8.hip): the golden fixtures within the
-    bound, and bitwise the int8-MFMA path's embeddings (BERT_AMD_I8=1)."""
-    meta, toks, want = load_case(case)
-    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    outs = {}
-    for f6 in ("1", "0"):
-        monkeypatch.setenv("BERT_AMD_F6", f6)
-        monkeypatch.setenv("BERT_AMD_I8", "1")
-        m = bertlib.BertModel(p)  # fresh context: both are read at load
-        try:
-            outs[f6] = m.eval_batch(toks)
-            assert np.array_equal(outs[f6], m.eval_batch(toks))
-        finally:
-            m.close()
-    c = cos(outs["1"], want)
-    print(f"BERT_AMD_F6=1 {case}: 1-cos max {1 - c.min():.2e}")
-    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
-    assert np.array_equal(outs["1"], outs["0"])
 
 
 def test_batch_invariance_and_determinism(model_dir):
@@ -510,7 +387,7 @@ def test_mixed_lengths_group_like_separate_batches(model_dir):
 
 
 @pytest.mark.parametrize("shape,ftype,n_layer,vocab", [("e5-base", "f16", None, 250002), ("bge-large", "q4_1", 2, 30522)])
-def test_packed_head_dim_64_equal_alone(shape, ftype, n_layer, vocab, model_dir, monkeypatch):
+def test_packed_head_dim_64_equal_alone(shape, ftype, n_layer, vocab, model_dir):
     """Packed fused tiles at head dim 64 (e5-base f16, bge-large Q4_1 with 2
     layers; packing forced): every sentence equals itself evaluated alone,
     bitwise."""
@@ -530,7 +407,7 @@ def test_packed_head_dim_64_equal_alone(shape, ftype, n_layer, vocab, model_dir,
 
 @pytest.mark.parametrize("ftype", ["q4_0", "f16"])
 @pytest.mark.parametrize("pack", ["1", "auto"])
-def test_packed_short_sentences_equal_alone(ftype, pack, model_dir, monkeypatch):
+def test_packed_short_sentences_equal_alone(ftype, pack, model_dir):
     """Short sentences share a fused QKV+attention workgroup (runtime.cpp packs
     consecutive sentences while their lengths rounded up to 32 sum to <= 128;
     1 to 4 per tile; "auto" packs when it saves workgroup rounds, which this
@@ -586,15 +463,13 @@ def test_device_batch_reordered_into_tiles(model_dir):
         assert np.array_equal(dev[i], m.eval(toks[i])), i
 
 
-@pytest.mark.parametrize("i8", ["default", "0"])
-def test_half_row_ln_tiles(i8, model_dir, monkeypatch):
+@pytest.mark.parametrize("i8", ["", "0"])
+def test_half_row_ln_tiles(i8, model_dir):
     """A batch whose 128-row LN GEMM tiles would leave the last round of
     workgroups mostly empty runs 64-row tiles (kernels.hip ln_half_rows):
     per-sentence results equal the sentences alone, bitwise."""
-    if i8 != "default":
-        monkeypatch.setenv("BERT_AMD_I8", i8)
     p, _ = get_model(model_dir, "minilm", "q4_0")
-    m = bertlib.BertModel(p)  # fresh context: BERT_AMD_I8 is read at load
+    m = bertlib.BertModel(p, options={"i8": i8} if i8 else None)  # fresh context: i8 is a load option
     try:
         rng = np.random.default_rng(11)
         toks = [[101] + rng.integers(1000, 30522, 98).tolist() + [102] for _ in range(400)]  # 40 000 rows
