@@ -29,6 +29,9 @@ $(BUILD)/obj/%.o: $(SRC)/%.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
 
 $(BUILD)/libbert.so: $(HOST_OBJS) $(HIP_OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+	@# the commit this library was built from (bench.py / tools/pmc_traffic.py record it)
+	@{ git rev-parse HEAD 2>/dev/null || echo unknown; } | tr -d '\n' > $(BUILD)/BUILD_INFO
+	@git diff --quiet HEAD -- embedding.cpp_amd include 2>/dev/null || printf ' +uncommitted' >> $(BUILD)/BUILD_INFO
 
 oracle:
 	$(MAKE) -C oracle
@@ -85,3 +88,13 @@ $(BUILD)/qkva_time: tools/qkva_time.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SR
 $(BUILD)/pmc_calib: tools/pmc_calib.hip
 	@mkdir -p $(BUILD)
 	$(HIPCC) -O3 --offload-arch=gfx950 $< -o $@
+
+# development per-phase stamps of the persistent int8 GEMMs (tools/phase_stamps.hip)
+$(BUILD)/phase_stamps: tools/phase_stamps.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $< -o $@
+
+# the fused kernel's phase stamps (tools/qkva_time.hip -DPHASE_STAMPS)
+$(BUILD)/qkva_stamps: tools/qkva_time.hip tools/stamps.h $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DPHASE_STAMPS=1 $< -o $@

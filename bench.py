@@ -35,7 +35,7 @@ METRIC = "embeddings/sec at seq_len=128 batch=1024; cosine-sim vs ggml CPU ref"
 PEAK_FP16_TFLOPS = 2516.6  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFLOPS = 157.3
 PEAK_INT8_TOPS = 2 * PEAK_FP16_TFLOPS  # i8 MFMA: 2x the bf16 rate per clock (MI355X_MICROARCH.md MFMA table)
-I8_KERNELS = ("gemm_up_gelu", "gemm_down_ln", "gemm_ffn_ln")  # the int8-MFMA GEMMs of the Q4 models
+I8_KERNELS = ("gemm_up_gelu", "gemm_down_ln")  # the int8-MFMA GEMMs of the Q4 models
 PEAK_HBM_GBS = 8000.0
 
 
@@ -78,6 +78,64 @@ def max_over_ranks(x: float, device=None) -> float:
     return float(t.item())
 
 
+def library_sharding(rank: int, world: int, cpu_barrier, work):
+    """bench's N > 1 library-sharding step (reference bert.cpp:1065: sentences are
+    independent): rank 0 runs `work()` — bert_amd_load over every device of the
+    node + bert_eval_batch on the global batch — while the other ranks wait in
+    `cpu_barrier` (a gloo barrier: it blocks on the CPU, so the waiting ranks do
+    not spin on their GPUs the way an RCCL barrier would, and it fails with a
+    timeout error instead of hanging if rank 0 dies).  Returns work()'s result
+    on rank 0, None elsewhere."""
+    res = None
+    try:
+        if rank == 0:
+            res = work()
+    finally:
+        cpu_barrier()
+    return res
+
+
+def lib_shard_work(model_cls, path, devices, gtoks, B, out_rank0, workload):
+    """Rank 0's part of library_sharding: time bert_eval_batch over the global
+    batch (host buffers, median of 5 after 2 warm-ups) on a context replicated
+    over `devices`, and check its first B rows against rank 0's own shard."""
+    gm = model_cls(path, devices=devices)
+    try:
+        run, gemb = gm.prepared_batch(list(gtoks))
+        for _ in range(2):
+            run()
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            run()
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        n = len(gtoks)
+        return dict(value=round(n / med, 1), unit="embeddings/s", devices=gm.n_devices, workload=workload,
+                    ms_median=round(med * 1e3, 3), runs=5, bitwise_vs_rank0=bool(np.array_equal(gemb[:B], out_rank0)),
+                    note="bert_amd_load(devices=0..N-1) + bert_eval_batch on host buffers "
+                         "(H2D ids and D2H embeddings included)")
+    finally:
+        gm.close()
+
+
+def build_info() -> dict:
+    """The library this run measures: sha256 of build/libbert.so and the git
+    HEAD it was built from (build/BUILD_INFO, written by make)."""
+    import hashlib
+    info = {}
+    try:
+        with open(bertlib.LIB_PATH, "rb") as f:
+            info["lib_sha256"] = hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        pass
+    bi = os.path.join(os.path.dirname(bertlib.LIB_PATH), "BUILD_INFO")
+    if os.path.exists(bi):
+        with open(bi) as f:
+            info["git_head"] = f.read().strip()
+    return info
+
+
 def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
     E, I = hp["n_embd"], hp["n_intermediate"]
     M = B * N
@@ -86,7 +144,6 @@ def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
         "gemm_o_ln": 2.0 * M * E * E,
         "gemm_up_gelu": 2.0 * M * E * I,
         "gemm_down_ln": 2.0 * M * I * E,
-        "gemm_ffn_ln": 4.0 * M * E * I,
         "attention": 4.0 * B * N * N * E,
         "qkv_attention": 2.0 * M * E * 3 * E + 4.0 * B * N * N * E,
     }.get(name, 0.0)
@@ -103,7 +160,6 @@ def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
         "gemm_o_ln": M * E * act + E * E * wb + 2 * M * E * 4 + M * E * act,
         "gemm_up_gelu": M * E * act + E * I * wb + M * I * act,
         "gemm_down_ln": M * I * act + E * I * wb + 2 * M * E * 4 + M * E * act,
-        "gemm_ffn_ln": M * E * act + 2 * E * I * wb + 2 * M * E * 4 + M * E * act,  # U stays on chip
         "attention": M * 3 * E * 4 + M * E * act,
         "qkv_attention": M * E * act + 3 * E * E * wb + M * E * act,
         "embed_ln": M * 4 + M * E * (4 + act) + M * E * 4,  # f32 word rows (pos/type tables stay cached)
@@ -136,7 +192,7 @@ def pmc_traffic(csv_path: str, kernel_substr: str):
 # name fragments of the dominant kernels' mangled symbols (for PMC CSV lookup)
 KERNEL_SYMBOL = {
     "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "i8_up_gelu_kernel",
-    "gemm_down_ln": "i8_ln384_kernel", "gemm_ffn_ln": "i8_ffn384_kernel", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
+    "gemm_down_ln": "i8_ln384_kernel", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
     "pool_l2": "pool_l2_kernel",
 }
 
@@ -241,12 +297,16 @@ def main():
     gpu = 0 if args.rehearse_one_gpu else local_rank
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    cpu_group = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
         if args.rehearse_one_gpu:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+            # CPU-side waits (library_sharding) go through gloo, not RCCL
+            cpu_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=20))
 
     def barrier():
         if world > 1:
@@ -348,34 +408,38 @@ def main():
             roofline = dict(kernel=dominant, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                             frac=round(ach / PEAK_HBM_GBS, 4), bytes_per_launch=by)
         traffic, tsrc = None, None
-        if args.pmc_csv:
-            traffic = pmc_traffic(args.pmc_csv, KERNEL_SYMBOL.get(dominant, dominant))
-            tsrc = args.pmc_csv
-        else:
-            # corrected FETCH_SIZE x2 + WRITE_SIZE per launch measured by tools/profile_round.sh on
-            # this code for this workload (separate rocprofv3 --pmc passes; profiles/)
-            pf = os.path.join(REPO, "profiles", "pmc_traffic.json")
-            if os.path.exists(pf):
-                with open(pf) as f:
-                    pt = json.load(f)
-                wl = f"{args.shape} {args.ftype} batch={B} seq_len={N}"
-                if pt.get("workload") == wl and dominant in pt.get("bytes_per_launch", {}):
-                    traffic = pt["bytes_per_launch"][dominant]
-                    tsrc = f"profiles/pmc_traffic.json ({pt.get('source', '')})"
-        roofline["traffic"] = traffic
-        roofline["traffic_source"] = tsrc
-        # whole-step achieved HBM (north_star): PMC bytes of one step's launches
-        # (profiles/pmc_traffic.json bytes_per_step) over this run's ms_per_step
+        # profiles/pmc_traffic.json: corrected FETCH_SIZE x2 + WRITE_SIZE per launch
+        # measured by tools/profile_round.sh (separate rocprofv3 --pmc passes) on the
+        # library it records (lib_sha256, git_head); it is used only for the same
+        # workload, and marked stale when this run's library is a different build
+        pt, stale = None, None
         pf = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(pf):
             with open(pf) as f:
                 pt = json.load(f)
-            if pt.get("workload") == f"{args.shape} {args.ftype} batch={B} seq_len={N}" and pt.get("bytes_per_step"):
-                bps = float(pt["bytes_per_step"])
-                gbs = bps / (ms_per_step * 1e-3) / 1e9
-                hbm_step = dict(bytes_per_step=round(bps), achieved_GBs=round(gbs, 1), peak_GBs=PEAK_HBM_GBS,
-                                frac=round(gbs / PEAK_HBM_GBS, 4),
-                                source=f"profiles/pmc_traffic.json ({pt.get('source', '')}) over this run's ms_per_step")
+            if pt.get("workload") != f"{args.shape} {args.ftype} batch={B} seq_len={N}":
+                pt = None
+            else:
+                stale = pt.get("lib_sha256") != build_info().get("lib_sha256")
+        if args.pmc_csv:
+            traffic = pmc_traffic(args.pmc_csv, KERNEL_SYMBOL.get(dominant, dominant))
+            tsrc = args.pmc_csv
+        elif pt and dominant in pt.get("bytes_per_launch", {}):
+            traffic = pt["bytes_per_launch"][dominant]
+            tsrc = (f"profiles/pmc_traffic.json ({pt.get('source', '')}; git {pt.get('git_head', '?')})"
+                    + (" STALE: measured on a different build of libbert.so" if stale else ""))
+        roofline["traffic"] = traffic
+        roofline["traffic_source"] = tsrc
+        roofline["traffic_stale"] = bool(stale) if (traffic is not None and not args.pmc_csv) else False
+        # whole-step achieved HBM (north_star): PMC bytes of one step's launches
+        # (profiles/pmc_traffic.json bytes_per_step) over this run's ms_per_step
+        if pt and pt.get("bytes_per_step"):
+            bps = float(pt["bytes_per_step"])
+            gbs = bps / (ms_per_step * 1e-3) / 1e9
+            hbm_step = dict(bytes_per_step=round(bps), achieved_GBs=round(gbs, 1), peak_GBs=PEAK_HBM_GBS,
+                            frac=round(gbs / PEAK_HBM_GBS, 4), stale=bool(stale),
+                            source=f"profiles/pmc_traffic.json ({pt.get('source', '')}; git {pt.get('git_head', '?')}) "
+                                   f"over this run's ms_per_step")
         roofline["algorithmic_bytes_per_launch"] = kernel_bytes(dominant, B, N, hp, args.ftype)
 
     # whole-path MFMA fraction: F(N) = L(8NE^2 + 4NEI + 4N^2E) per sentence
@@ -501,37 +565,14 @@ def main():
     # global batch world x B; rank 0 only, the other ranks idle on the CPU
     lib_shard = None
     if world > 1 and args.lib_shard:
-        flag = f"/tmp/bert_amd_libshard_{os.environ.get('MASTER_PORT', '0')}.done"
+        import torch.distributed as dist
         if rank == 0:
             log(f"library sharding over {world} devices")
-            gm = bertlib.BertModel(path, devices=[0] * world if args.rehearse_one_gpu else list(range(world)))
-            try:
-                gtoks = splitmix_tokens(0, world * B, N, hp["n_vocab"])
-                run, gemb = gm.prepared_batch(list(gtoks))
-                for _ in range(2):
-                    run()
-                ts = []
-                for _ in range(5):
-                    t0 = time.perf_counter()
-                    run()
-                    ts.append(time.perf_counter() - t0)
-                med = float(np.median(ts))
-                lib_shard = dict(value=round(world * B / med, 1), unit="embeddings/s", devices=gm.n_devices,
-                                 workload=f"{args.shape} {args.ftype} global batch={world * B} seq_len={N}",
-                                 ms_median=round(med * 1e3, 3), runs=5,
-                                 bitwise_vs_rank0=bool(np.array_equal(gemb[:B], out)),
-                                 note="bert_amd_load(devices=0..N-1) + bert_eval_batch on host buffers "
-                                      "(H2D ids and D2H embeddings included)")
-            finally:
-                gm.close()
-                with open(flag, "w") as f:
-                    f.write("done")
-        else:
-            while not os.path.exists(flag):
-                time.sleep(0.05)
-        barrier()
-        if rank == 0:
-            os.remove(flag)
+        devices = [0] * world if args.rehearse_one_gpu else list(range(world))
+        lib_shard = library_sharding(
+            rank, world, lambda: dist.barrier(group=cpu_group),
+            lambda: lib_shard_work(bertlib.BertModel, path, devices, splitmix_tokens(0, world * B, N, hp["n_vocab"]),
+                                   B, out, f"{args.shape} {args.ftype} global batch={world * B} seq_len={N}"))
 
     if rank == 0:
         res = {
@@ -549,6 +590,7 @@ def main():
                        else f"{args.shape} shape, synthetic weights",
                        "global_batch": B * world, "seq_len": N, "parallelism": f"dp{world}"},
             "roofline": roofline,
+            "build": build_info(),
             "pipeline_mfma_frac": round(path_frac, 4),
             "step_hbm": hbm_step,
             "kernels": kern,

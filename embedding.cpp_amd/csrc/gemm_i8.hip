@@ -277,14 +277,21 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
     }
 }
 
+struct I8NoHook {
+    __device__ __forceinline__ void operator()(int, int) const {}
+};
+
 // acc[f][t] = A[m0 + 32 (tt0 + t) ..][:] . W[32 (ft0 + f) ..][:]^T over the
 // whole K for this wave's F f-tiles x T t-tiles (tokens of the workgroup's
 // BM-row tile, staged through `smem`, 2 * I8Chunk::BYTES).  `pp` holds this
 // tile's first loads on entry (I8Pipe::prime) and the next tile's (m0n,
 // ft0n) on return.  Returns after a final barrier (the LDS may be reused).
-template <int WT, int NT, int BM, int F, int T, bool PIPE = true>
+// hook(c, nch) runs at the start of every chunk c, after that chunk's barrier
+// (memory traffic of the caller's epilogue interleaved with the main loop).
+template <int WT, int NT, int BM, int F, int T, bool PIPE = true, typename Hook = I8NoHook>
 __device__ __forceinline__ void i8_mainloop(const GemmArgs &g, int64_t m0, int ft0, int tt0, int64_t m0n, int ft0n,
-                                            char *smem, I8Pipe<WT, NT, BM, F> &pp, float16v (&acc)[F][T]) {
+                                            char *smem, I8Pipe<WT, NT, BM, F> &pp, float16v (&acc)[F][T],
+                                            const Hook &hook = Hook()) {
     constexpr bool Q1 = WT == W_Q4_1;
     using C = I8Chunk<BM, Q1>;
     const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -316,6 +323,7 @@ __device__ __forceinline__ void i8_mainloop(const GemmArgs &g, int64_t m0, int f
         const bool more = c + 1 < nch;
         const int b0 = 4 * c;
         const char *buf = smem + (c & 1) * C::BYTES;
+        hook(c, nch);
         I8AOps<T> a0, a1;
         i8_aops<WT, BM, T, 0>(a0, buf, tt0);
         i8_block<WT, BM, F, T, 0, PIPE>(buf, tt0, pp.wf[0], ws, wd, wm, a0, a1, acc);
@@ -402,12 +410,14 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
     coords(blockIdx.x, m0, ft0);
     I8Pipe<WT, NT, BM, F> pp;
     pp.prime(g, m0, ft0);
-    for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
+    for (int tile = blockIdx.x, it = 0; tile < nwg; tile += gridDim.x, it++) {
         int64_t m0n = m0;
         int ft0n = ft0;
         if (tile + (int)gridDim.x < nwg) coords(tile + gridDim.x, m0n, ft0n);
         float16v acc[F][T];
+        STAMP(it, 0, NWV);
         i8_mainloop<WT, NT, BM, F, T, PIPE>(g, m0, ft0, tw, m0n, ft0n, smem, pp, acc);
+        STAMP(it, 1, NWV);
         const int64_t mc = m0;
         const int fc = ft0;
         m0 = m0n;
@@ -430,6 +440,7 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
                 i8_store_q8_half<WT>(g.out_act, g.N, mc + 32 * (tw + t) + l32, fc + f, hh, y);
             }
         }
+        STAMP(it, 2, NWV);
     }
 }
 
@@ -446,9 +457,18 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
 // threads — instead of each lane gathering and scattering its own row (32
 // cache lines per wave instruction).  16-byte chunk c of row r sits at LDS
 // chunk c ^ (r & 15), so the epilogue's row-per-lane reads are conflict-free.
+// With OV (I8_LN_OV, default) that traffic overlaps the main loops: the tile's
+// residual comes in piece by piece during its own main loop (LDS-DMA issued at
+// the chunk starts), and the previous tile's LN output leaves xs during the same
+// chunks, each wave draining one 1 KiB piece of xs to X just before refilling
+// that piece with the new residual; the last tile's output leaves after the loop.
 __device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ (r & 15)); }
 
-template <int WT>
+#ifndef I8_LN_OV
+#define I8_LN_OV 1
+#endif
+
+template <int WT, bool OV = I8_LN_OV>
 __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles) {
     constexpr int NT = 768, BM = 64, F = 1, T = 2, NCOL = 384, NWV = 12;
     constexpr int XCH = BM * NCOL / 4;  // 16-byte chunks of the residual tile
@@ -463,22 +483,56 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
     int64_t m0n = (int64_t)xcd_linear(blockIdx.x, n_mtiles) * BM;
     I8Pipe<WT, NT, BM, F> pp;
     pp.prime(g, m0n, ft0);
-    for (int tile = blockIdx.x; tile < n_mtiles; tile += gridDim.x) {
+    // wave w's piece k: LDS chunks 64 (8 w + k) .. + 63 of xs, i.e. lane l holds
+    // chunk j = 64 (8 w + k) + l = (row r, column chunk cs ^ (r & 15)) of the tile
+    constexpr int PIECES = XCH / NT;  // 1 KiB pieces per wave
+    auto piece_off = [&](int k, int &j0) {
+        j0 = 64 * (8 * wv + k);
+        const int j = j0 + lane, r = j / 96, cs = j - 96 * r;
+        return r * NCOL + 4 * (cs ^ (r & 15));
+    };
+    auto dma_in = [&](const float *xt, int k) {
+        int j0;
+        const int off = piece_off(k, j0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(xt + off),
+                                         (__attribute__((address_space(3))) void *)(xs + 4 * j0), 16, 0, 0);
+    };
+    auto store_out = [&](float *xt, int k) {
+        int j0;
+        const int off = piece_off(k, j0);
+        *(float4v *)(xt + off) = *(const float4v *)(xs + 4 * (j0 + lane));
+    };
+    int64_t mprev = -1;
+    for (int tile = blockIdx.x, it = 0; tile < n_mtiles; tile += gridDim.x, it++) {
         const int64_t m0 = m0n;
         if (tile + (int)gridDim.x < n_mtiles) m0n = (int64_t)xcd_linear(tile + gridDim.x, n_mtiles) * BM;
         float16v acc[F][T];
-        i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc);
-        {   // residual tile -> xs: wave w's LDS-DMA k covers LDS chunks 64 (8 w + k) ..
-            const float *xt = g.X + m0 * NCOL;
+        STAMP(it, 0, NWV);
+        if constexpr (OV) {
+            // chunk c drains and refills pieces c ppc .. (previous output out, this residual in)
+            const float *xin = g.X + m0 * NCOL;
+            float *xout = g.X + mprev * NCOL;
+            const bool prev = mprev >= 0;
+            auto hook = [&](int c, int nch) {
+                const int ppc = (PIECES + nch - 1) / nch, k1 = min(PIECES, (c + 1) * ppc);
 #pragma unroll 1
-            for (int k = 0; k < XCH / NT; k++) {
-                const int j0 = 64 * (8 * wv + k), j = j0 + lane, r = j / 96, cs = j - 96 * r;
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)(xt + r * NCOL + 4 * (cs ^ (r & 15))),
-                    (__attribute__((address_space(3))) void *)(xs + 4 * j0), 16, 0, 0);
-            }
+                for (int k = c * ppc; k < k1; k++) {
+                    if (prev) store_out(xout, k);
+                    dma_in(xin, k);
+                }
+            };
+            i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc, hook);
+        } else {
+            i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc);
         }
-        __syncthreads();  // (drains the LDS-DMA: vmcnt(0) before the barrier)
+        STAMP(it, 1, NWV);
+        if constexpr (!OV) {  // residual tile -> xs
+#pragma unroll 1
+            for (int k = 0; k < PIECES; k++) dma_in(g.X + m0 * NCOL, k);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
+        __syncthreads();                                   // ... and every other wave's
+        STAMP(it, 2, NWV);
         // v = (b + W.x) + x  (ggml: add(repeat(b), mul_mat) then add(cur, inpL))
 #pragma unroll
         for (int t = 0; t < T; t++) {
@@ -499,6 +553,7 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
             if (hh == 0) red[0][wv][r] = s;
         }
         __syncthreads();
+        STAMP(it, 3, NWV);
         float mean[T];
 #pragma unroll
         for (int t = 0; t < T; t++) {
@@ -518,6 +573,7 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
             if (hh == 0) red[1][wv][r] = s2;
         }
         __syncthreads();
+        STAMP(it, 4, NWV);
 #pragma unroll
         for (int t = 0; t < T; t++) {
             const int r = 32 * t + l32;
@@ -544,17 +600,24 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
             }
             i8_store_q8_half<WT>(g.out_act, NCOL, row, ft0, hh, y);
         }
-        __syncthreads();
-        {   // xs -> X: consecutive threads store consecutive 16-byte chunks
-            float *xt = g.X + m0 * NCOL;
+        STAMP(it, 5, NWV);
+        mprev = m0;
+        if constexpr (!OV) {
+            __syncthreads();
+            STAMP(it, 6, NWV);
 #pragma unroll 1
-            for (int k = 0; k < XCH / NT; k++) {
-                const int j = tid + NT * k, r = j / 96, cs = j - 96 * r;
-                *(float4v *)(xt + r * NCOL + 4 * (cs ^ (r & 15))) = *(const float4v *)(xs + 4 * j);
-            }
+            for (int k = 0; k < PIECES; k++) store_out(g.X + m0 * NCOL, k);  // xs -> X
+            STAMP(it, 7, NWV);
         }
-        // the next tile's main loop reuses `red` and its LDS-DMA rewrites xs only
-        // after the main loop's own barriers
+        // the next tile's main loop reuses `red` and rewrites xs (pieces) only
+        // after the main loop's first barrier
+    }
+    if constexpr (OV) {  // the last tile's LN output
+        __syncthreads();
+        if (mprev >= 0) {
+#pragma unroll 1
+            for (int k = 0; k < PIECES; k++) store_out(g.X + mprev * NCOL, k);
+        }
     }
 }
 

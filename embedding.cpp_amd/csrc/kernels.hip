@@ -1373,12 +1373,14 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
         // plays the one-unit role of the split below.
         const int64_t nt0 = (int64_t)qd * NTW * NW + NTW * wv;
         float4v acc[RT][NTW];
+        STAMP(qd, 0, NW);
         MainloopPre<WT, NW, BM, NTW, QKB> pre;
         mainloop_preload(pre, g, beg, nt0);
         if (part_w == 2)  // ends with a barrier
             gemm_mainloop<WT, NW, BM, NTW, false, QKB>(g, beg, nt0, smem, acc, pre);
         else
             gemm_mainloop<WT, NW, BM, NTW, true, QKB>(g, beg, nt0, smem, acc, pre);
+        STAMP(qd, 1, NW);
 #pragma unroll
         for (int half = 0; half < NTW; half++) {
             const int pr = NTW * qd + half;
@@ -1449,6 +1451,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                 }
             }
             __syncthreads();
+            STAMP(qd, 2 + 2 * half, NW);
 
             if (wv < 8) {  // attention task (head slot or dim half, query block: 32 queries of one sentence)
                 const int hs = HU == 2 ? wv >> 2 : 0, qb = wv & 3, head = HU * pr + hs;
@@ -1538,6 +1541,7 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
                 }
             }
             __syncthreads();  // the next pair's tiles / the next quad's A chunks overwrite the attention tiles
+            STAMP(qd, 3 + 2 * half, NW);
         }
     }
 }

@@ -16,6 +16,25 @@ typedef _Float16 half4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));  // 16 raw bytes as a register vector
 typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 
+// Development phase stamps (tools/phase_stamps.hip): compiled out of the
+// library; with -DPHASE_STAMPS lane 0 of waves 0 and NW - 1 of each
+// workgroup records s_memtime (shader cycles) per persistent-tile iteration
+// and slot into g_stamp_buf[((blockIdx.x * STAMP_TILES + it) * 2 + w) * 16 + slot].
+#ifdef PHASE_STAMPS
+constexpr int STAMP_TILES = 32;
+static __device__ unsigned long long *g_stamp_buf;  // set by the tool before any launch
+static __device__ int g_stamp_nblk;                 // workgroups the buffer holds
+#define STAMP(it, slot, nw)                                                                                     \
+    do {                                                                                                        \
+        const int w_ = threadIdx.x >> 6;                                                                        \
+        if ((threadIdx.x & 63) == 0 && (w_ == 0 || w_ == (nw) - 1) && (it) < STAMP_TILES && g_stamp_buf &&      \
+            (int)blockIdx.x < g_stamp_nblk)                                                                     \
+            g_stamp_buf[((blockIdx.x * STAMP_TILES + (it)) * 2 + (w_ != 0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(it, slot, nw) ((void)0)
+#endif
+
 __device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 

@@ -4,7 +4,9 @@ MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE counts half of the
 bytes of wide coalesced reads: doubled; both counters in KB), written as
 profiles/pmc_traffic.json for bench.py's roofline.traffic.
 python tools/pmc_traffic.py <fetch dir> <write dir> <workload> <out.json> [source note]"""
+import hashlib
 import json
+import os
 import sys
 
 sys.path.insert(0, __file__.rsplit("/", 1)[0])
@@ -17,7 +19,6 @@ NAMES = {
     # default C3 build: o-proj on the split-fp16 LN GEMM, down on the int8 one
     "gemm_o_ln": ["gemm_kernelILi2ELi2", "gemm_kernel<2, 2,", "i8_ln384_kernel"],
     "gemm_down_ln": ["i8_ln384_kernel", "gemm_kernelILi2ELi2", "gemm_kernel<2, 2,"],
-    "gemm_ffn_ln": ["i8_ffn384_kernel"],
     "embed_ln": ["embed_ln_kernel"],
     "pool_l2": ["pool_l2_kernel"],
 }
@@ -29,6 +30,17 @@ def main():
            "fetch_bytes": {}, "write_bytes": {},
            "note": "FETCH_SIZE x2 + WRITE_SIZE, KB -> bytes, per dispatch; each name takes the kernels of "
                    "its first symbol fragment that occurs (o-proj: split-fp16 LN GEMM, down: int8 LN GEMM)"}
+    # the build these counters describe (bench.py marks the traffic stale for any other build)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(repo, "build", "libbert.so")
+    if os.path.exists(lib):
+        with open(lib, "rb") as f:
+            out["lib_sha256"] = hashlib.sha256(f.read()).hexdigest()
+    bi = os.path.join(repo, "build", "BUILD_INFO")
+    if os.path.exists(bi):
+        with open(bi) as f:
+            out["git_head"] = f.read().strip()
+    out["kernel_symbols"] = sorted(set(fetch) | set(write))
     for name, frags in NAMES.items():
         fv, wv = [], []
         keys = set(fetch) | set(write)
@@ -46,11 +58,9 @@ def main():
             out["write_bytes"][name] = round(wb)
             out["bytes_per_launch"][name] = round(fb + wb)
     # whole step: every layer kernel launches n_layer (6) times per step, embed and pool once
-    # (gemm_ffn_ln replaces up + down when the fused FFN kernel is on; otherwise absent)
     per_step = {"embed_ln": 1, "pool_l2": 1}
     bl = out["bytes_per_launch"]
-    step = [k for k in NAMES if k != "gemm_ffn_ln"] if "gemm_ffn_ln" not in bl else \
-        [k for k in NAMES if k not in ("gemm_up_gelu", "gemm_down_ln")]
+    step = list(NAMES)
     if all(k in bl for k in step):
         out["bytes_per_step"] = round(sum(bl[k] * per_step.get(k, 6) for k in step))
     with open(sys.argv[4], "w") as f:

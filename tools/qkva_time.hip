@@ -4,7 +4,13 @@
 // 384) and with the GEMM main loop emptied (K = 0: the attention phase, the
 // tile epilogues and the fixed per-workgroup costs only).
 //   build: make build/qkva_time      run: build/qkva_time [iters]
+// With -DPHASE_STAMPS (make build/qkva_stamps) it also prints the per-phase
+// cycle medians of one launch (kernels.hip STAMP slots: main loop, hi/lo split
+// into the attention tiles + barrier, attention + barrier, per head pair).
 #include "../embedding.cpp_amd/csrc/kernels.hip"
+#ifdef PHASE_STAMPS
+#include "stamps.h"
+#endif
 
 #include <cmath>
 #include <cstdio>
@@ -87,6 +93,15 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+#ifdef PHASE_STAMPS
+    // every launch of a stamped kernel writes the buffer: set it before the first one
+    const size_t n_st = (size_t)S * STAMP_TILES * 2 * 16;
+    unsigned long long *d_st;
+    CK(hipMalloc(&d_st, n_st * 8));
+    CK(hipMemset(d_st, 0, n_st * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &d_st, sizeof(d_st)));
+    { const int nb = S; CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_nblk), &nb, sizeof(nb))); }
+#endif
     for (int K : {E, 0}) {
         g.K = K;
         auto launch = [&] {
@@ -103,6 +118,17 @@ int main(int argc, char **argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         printf("qkv_attention q4_0 K=%d: %8.1f us\n", K, ms * 1000.0 / iters);
         fflush(stdout);
+#ifdef PHASE_STAMPS
+        if (K == E) {
+            CK(hipMemset(d_st, 0, n_st * 8));
+            launch();
+            CK(hipDeviceSynchronize());
+            std::vector<unsigned long long> h(n_st);
+            CK(hipMemcpy(h.data(), d_st, n_st * 8, hipMemcpyDeviceToHost));
+            const char *names[] = {"main", "split0", "attn0", "split1", "attn1", "->quad"};
+            stamp_report(h, S, STAMP_TILES, 6, names, ms * 1000.0 / iters);
+        }
+#endif
     }
     return 0;
 }
