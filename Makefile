@@ -23,7 +23,7 @@ $(BUILD)/obj/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/bert.h include/ber
 
 $(BUILD)/obj/tokenizer.o: $(SRC)/unicode_tables.inc
 
-$(BUILD)/obj/%.o: $(SRC)/%.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+$(BUILD)/obj/%.o: $(SRC)/%.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -52,12 +52,12 @@ $(BUILD)/div_check: tools/div_check.hip
 
 # development timing harness for the int8-MFMA GEMMs (not shipped)
 
-$(BUILD)/i8_bench$(I8_SUFFIX): tools/i8_bench.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+$(BUILD)/i8_bench$(I8_SUFFIX): tools/i8_bench.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 
 # development check of the fused kernel's head-pair grouping, F16 (tools/qkva_check.hip)
-$(BUILD)/qkva_check: tools/qkva_check.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+$(BUILD)/qkva_check: tools/qkva_check.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 
@@ -80,7 +80,7 @@ ref_consumers: $(BUILD)/ref_server $(BUILD)/ref_main
 .PHONY: ref_consumers
 
 # development timing of the fused kernel's phases (tools/qkva_time.hip)
-$(BUILD)/qkva_time: tools/qkva_time.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+$(BUILD)/qkva_time: tools/qkva_time.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 
@@ -90,11 +90,11 @@ $(BUILD)/pmc_calib: tools/pmc_calib.hip
 	$(HIPCC) -O3 --offload-arch=gfx950 $< -o $@
 
 # development per-phase stamps of the persistent int8 GEMMs (tools/phase_stamps.hip)
-$(BUILD)/phase_stamps: tools/phase_stamps.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+$(BUILD)/phase_stamps: tools/phase_stamps.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 
 # the fused kernel's phase stamps (tools/qkva_time.hip -DPHASE_STAMPS)
-$(BUILD)/qkva_stamps: tools/qkva_time.hip tools/stamps.h $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h
+$(BUILD)/qkva_stamps: tools/qkva_time.hip tools/stamps.h $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DPHASE_STAMPS=1 $< -o $@

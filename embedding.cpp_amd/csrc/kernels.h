@@ -156,7 +156,8 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles);
 // 64); g: the QKV GemmArgs (head-major weights in the kernel's grouped tile
 // order), a: the AttnArgs (its Q/K/V pointers unused).  ntw: 192-feature
 // units (head pairs at head dim 32) per GEMM main loop, 1 or 2 — the grouping
-// of the kernel's QKV weight copy (runtime.cpp), chosen per context at load.
+// of the kernel's QKV weight copy (runtime.cpp), chosen per context at load;
+// 0: the producer / consumer kernel (head dim 32, n_embd 384; plain tile order).
 bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw);
 // n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
 hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s);
@@ -176,7 +177,8 @@ bool gemm_ln_fused(int wtype, int N);  // false: EPI_RESID + launch_ln
 bool gemm_gelu_blk8(int wtype);
 
 // Q4 x Q8 GEMMs on the int8 MFMA (gemm_i8.hip): EPI_GELU_ACT (N % 256 == 0),
-// EPI_LN (N == 384), EPI_RESID (N % 256 == 0); K % 128 == 0; Mpad % 128 == 0.
+// EPI_LN (N == 384), EPI_RESID (N % 256 == 0), EPI_QKV (N % 384 == 0; the
+// head-major QKV weights of qkv_attention_pc_kernel); K % 128 == 0; Mpad % 128 == 0.
 bool i8_gemm_supported(int epi, int N, int K);
 hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
 

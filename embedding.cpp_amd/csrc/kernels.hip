@@ -12,6 +12,7 @@
 //
 // Compiled with -ffp-contract=off: every fused multiply-add below is explicit.
 #include "kernels_common.h"
+#include "i8_core.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -1546,9 +1547,253 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
     }
 }
 
+// QKV projection + attention with producer and consumer waves (Q4_0, head
+// dim 32, n_embd 384: MiniLM; reference bert.cpp:905-942).  One 10-wave
+// workgroup per sentence (or packed tile, PK, as qkv_attention_kernel).  The
+// sentence's 128-row Q8 panel is loaded into LDS once.  Waves 0-5 produce: for
+// head h they run the QKV projection of the head's 96 features on the int8
+// MFMA over the resident panel (i8_resident_mainloop: no barriers; wave w:
+// part w / 2 of Q | K | V, tokens 64 (w & 1) ..), then split b + W.x hi / lo
+// into the head's attention tiles.  Waves 6-9 consume: query block w - 6 of
+// the head finished in the previous period — the attention task of
+// qkv_attention_kernel.  Period p overlaps head p's projection with head
+// p - 1's attention; two barriers per period (the consumers are done with the
+// tiles; the tiles hold the next head).  LDS: the panel (58 KB), one head's
+// tiles (57 KB), the exp table (40 KB).
+constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
+
+template <bool PK>
+__global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
+    constexpr int WT = W_Q4_0, D = 32, NP = QKPC_NP, NW = QKPC_NW, BM = 128, NT = NW * 64;
+    constexpr int NK = 128, KST = D + 8, VST = NK + 4, E = 384, NKB = E / 32;
+    using C = I8Chunk<BM, false>;
+    constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
+    __shared__ __attribute__((aligned(16))) char apanel[(E / I8_KC) * C::BYTES];
+    __shared__ __attribute__((aligned(16))) char tiles[SLOT];
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
+    __shared__ int qtab[PK ? 4 : 1][4];     // query block -> {first tile row of its sentence, length, first query, vs}
+    __shared__ uint8_t vslot[PK ? NK : 1];  // tile row -> V^T key slot
+    const int s0 = PK ? a.tiles[2 * blockIdx.x] : (int)blockIdx.x;
+    const int ns = PK ? a.tiles[2 * blockIdx.x + 1] : 1;
+    const int beg = a.offsets[s0], n = a.offsets[s0 + ns] - beg;
+    if (n > NK || n <= 0 || ns > 4 || g.K != E || a.E != E) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the role branches are scalar
+    const int r = lane & 31, hh = lane >> 5;
+    const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
+    for (int i = tid; i < a.expt.n_pad / 8; i += NT) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
+    // the sentence's A panel: rows beg .. beg + 127 (rows past the batch are the
+    // workspace's zero spare rows), chunk c = blocks 4c .. 4c + 3 in I8Chunk layout
+    for (int it = tid; it < BM * NKB; it += NT) {
+        const int row = it / NKB, b = it - row * NKB, c = b >> 2, bb = b & 3;
+        const int4v *src = (const int4v *)((const int8_t *)g.A.q + (int64_t)(beg + row) * E + 32 * b);
+        char *buf = apanel + c * C::BYTES;
+        int4v *dst = (int4v *)(buf + row * I8_LDQ + 32 * bb);
+        dst[0] = src[0];
+        dst[1] = src[1];
+        ((uint16_t *)(buf + C::QB))[bb * BM + row] = ((const uint16_t *)g.A.d)[(int64_t)(beg + row) * NKB + b];
+    }
+    // the attention tiles start zero: rows / key slots no token writes stay zero for every head
+    for (int i = tid; i < SLOT / 16; i += NT) ((uint4 *)tiles)[i] = uint4{0u, 0u, 0u, 0u};
+    if (PK && tid < NK) {
+        int b = 0, vs = 0, qb_b = 0, qb_len = 0, qb_q = 0, qb_vs = 0, slt = 0;
+        for (int j = 0; j < ns; j++) {
+            const int e = a.offsets[s0 + j + 1] - beg, len = e - b, span = (len + 31) & ~31;
+            if (tid >= b && tid < e) slt = vs + tid - b;
+            if (32 * tid >= vs && 32 * tid < vs + span) {
+                qb_b = b;
+                qb_len = len;
+                qb_q = 32 * tid - vs;
+                qb_vs = vs;
+            }
+            b = e;
+            vs += span;
+        }
+        vslot[PK ? tid : 0] = (uint8_t)slt;
+        if (tid < 4) {
+            qtab[PK ? tid : 0][0] = qb_b;
+            qtab[PK ? tid : 0][1] = qb_len;
+            qtab[PK ? tid : 0][2] = qb_q;
+            qtab[PK ? tid : 0][3] = qb_vs;
+        }
+    }
+    __syncthreads();
+    auto plane = [&](int pl) -> _Float16 * {  // 0 Qh 1 Ql 2 Kh 3 Kl 4 Vh 5 Vl
+        return (_Float16 *)(pl < 4 ? tiles + pl * NK * KST * 2 : tiles + 4 * NK * KST * 2 + (pl - 4) * D * VST * 2);
+    };
+    const int H = a.H;
+    if (wv < NP) {
+        // ---- producer: f-tile 3 h + part (part = w / 2: Q, K, V of head h), tokens
+        // 64 (w & 1) .. + 63 as two 32-token t-tiles; lane (r, hh) holds token
+        // 32 t + r of its t-tile t, head dims 16 hh .. 16 hh + 15 (i8_core.h)
+        const int part = wv >> 1, tt0 = 2 * (wv & 1);
+        for (int p = 0; p <= H; p++) {
+            float16v acc[1][2];
+            if (p < H) i8_resident_mainloop<WT, BM, 1, 2>(g, apanel, 3 * p + part, tt0, acc);
+            STAMP(p, 1, NW);
+            __syncthreads();  // X: the consumers are done with head p - 1's tiles
+            if (p < H) {
+                const int f0 = p * 3 * D + part * D + 16 * hh;  // head-major feature of acc[..][0]
+                float bias[16];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
+                }
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int row = 32 * (tt0 + t) + r;  // tile row (token of the tile)
+                    if (row < n) {                       // rows >= n stay zero
+                        half8 hv[2], lv[2];
+#pragma unroll
+                        for (int i = 0; i < 16; i++) {
+                            const float y = bias[i] + acc[0][t][i];
+                            const _Float16 yh = (_Float16)y;
+                            hv[i >> 3][i & 7] = yh;
+                            lv[i >> 3][i & 7] = (_Float16)(y - (float)yh);
+                        }
+                        if (part < 2) {  // Q | K: row-major [token][dim]
+                            _Float16 *ph = plane(2 * part) + row * KST + 16 * hh, *pl = plane(2 * part + 1) + row * KST + 16 * hh;
+                            *(half8 *)ph = hv[0];
+                            *(half8 *)(ph + 8) = hv[1];
+                            *(half8 *)pl = lv[0];
+                            *(half8 *)(pl + 8) = lv[1];
+                        } else {  // V^T [dim][key slot]
+                            const int slot = PK ? (int)vslot[row] : row;
+                            _Float16 *ph = plane(4) + (16 * hh) * VST + slot, *pl = plane(5) + (16 * hh) * VST + slot;
+#pragma unroll
+                            for (int i = 0; i < 16; i++) {
+                                ph[i * VST] = hv[i >> 3][i & 7];
+                                pl[i * VST] = lv[i >> 3][i & 7];
+                            }
+                        }
+                    }
+                }
+            }
+            STAMP(p, 2, NW);
+            __syncthreads();  // Y: head p's tiles are complete
+            STAMP(p + 1, 0, NW);
+        }
+    } else {
+        // ---- consumer: query block qb of head p - 1 (32 queries of one sentence)
+        const int qb = wv - NP;
+        int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
+        asm volatile("" : "+v"(lim));
+        const _Float16 *Qh = plane(0), *Ql = plane(1), *Kh = plane(2), *Kl = plane(3), *Vh = plane(4), *Vl = plane(5);
+        for (int p = 0; p <= H; p++) {
+            const int head = p - 1;
+            int kb = 0, len = n, qrel = 32 * qb, vs = 0;
+            if constexpr (PK) {
+                kb = qtab[qb][0];
+                len = qtab[qb][1];
+                qrel = qtab[qb][2];
+                vs = qtab[qb][3];
+            }
+            const bool act = head >= 0 && (PK ? len > 0 : qrel < n);
+            const int qrow = kb + qrel + r;  // tile row of this lane's query (rows past the sentence
+                                             // read finite LDS data; never stored)
+            float16v o[1];
+            uint32_t sum = 0;
+            if (act) {
+                const int nkt = (len + 31) >> 5;
+                int klim = lim;  // key 32 kt + (j & 3) + 8 (j >> 2) + 4 hh valid while < len
+                if constexpr (PK) {
+                    klim = len - 4 * hh;
+                    asm volatile("" : "+v"(klim));
+                }
+                half8 qh[D / 16], ql[D / 16];
+#pragma unroll
+                for (int ks = 0; ks < D / 16; ks++) {
+                    qh[ks] = *(const half8 *)(Qh + qrow * KST + 16 * ks + 8 * hh);
+                    ql[ks] = *(const half8 *)(Ql + qrow * KST + 16 * ks + 8 * hh);
+                }
+                auto scores = [&](int kt) {
+                    float16v S = attn_qk<D>(Kh, Kl, KST, kb + 32 * kt, r, hh, qh, ql);
+                    if (32 * kt + 32 > len) {
+#pragma unroll
+                        for (int j = 0; j < 16; j++)
+                            if (32 * kt + (j & 3) + 8 * (j >> 2) >= klim) S[j] = -INFINITY;
+                    }
+                    return S;
+                };
+                // pass 1: max of the unscaled K.Q (x -> fl(x * scale) is monotonic, so
+                // fl(max * scale) is ggml's max of the scaled scores).  Two key tiles at
+                // a time: their MFMA chains are independent, so one covers the
+                // other's latency (a consumer wave is alone in its role on its SIMD)
+                float mx = -INFINITY;
+                for (int kt = 0; kt < nkt; kt += 2) {
+                    const float16v S = scores(kt);
+                    if (kt + 1 < nkt) {
+                        const float16v S1 = scores(kt + 1);
+#pragma unroll
+                        for (int j = 0; j < 16; j++) mx = fmaxf(mx, S1[j]);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
+                }
+                mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
+                const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
+                // pass 2: p = exp_tab[fp16(s - max)], the exact integer sum of p * 2^24, V.P
+                // (key tiles in order into o; two tiles' scores and softmax in flight)
+                auto softmax = [&](const float16v &S, half8 (&ph)[2]) {
+#pragma unroll
+                    for (int j = 0; j < 16; j += 2) {
+                        const float2v d2 = mx2 - float2v{S[j], S[j + 1]} * sc2;
+                        uint16_t pb[2];
+#pragma unroll
+                        for (int e = 0; e < 2; e++) {
+                            const uint32_t hm = f2h(d2[e]);
+                            pb[e] = etab[epos + min(hm, (uint32_t)eneg)];
+                            ph[(j + e) >> 3][(j + e) & 7] = __builtin_bit_cast(_Float16, pb[e]);
+                        }
+                        const float2v pp = float2v{h2f(pb[0]), h2f(pb[1])} * float2v{16777216.0f, 16777216.0f};
+                        sum += (uint32_t)pp[0] + (uint32_t)pp[1];
+                    }
+                };
+                o[0] = float16v{};
+                for (int kt = 0; kt < nkt; kt += 2) {
+                    const bool two = kt + 1 < nkt;
+                    const float16v S = scores(kt);
+                    float16v S1;
+                    if (two) S1 = scores(kt + 1);
+                    half8 ph[2], ph1[2];
+                    softmax(S, ph);
+                    attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph, 0);
+                    if (two) {
+                        softmax(S1, ph1);
+                        attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt + 32, r, hh, ph1, 0);
+                    }
+                }
+            }
+            STAMP(p, 1, NW);
+            __syncthreads();  // X: this head's tiles may be overwritten
+            if (act) {
+                sum += __shfl_xor(sum, 32);
+                int orow = qrow;
+                asm volatile("" : "+v"(orow));
+                attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, head,
+                                         hh, 0);
+            }
+            STAMP(p, 2, NW);
+            __syncthreads();  // Y
+            STAMP(p + 1, 0, NW);
+        }
+    }
+}
+
 template <int WT, int D>
 static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s) {
     const bool pk = a.tiles != nullptr;
+    if constexpr (D == 32 && WT == W_Q4_0) {
+        if (ntw == 0) {  // producer / consumer waves (qkv_attention_pc_kernel; g.Wi: int8 QKV weights)
+            if (pk)
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<true>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a);
+            else
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<false>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a);
+            return hipGetLastError();
+        }
+    }
     if (ntw == 2) {
         if (pk)
             hipLaunchKernelGGL((qkv_attention_kernel<WT, D, 2, true>), dim3(n_blocks), dim3(QKVA_NW * 64), 0, s, g, a);
@@ -1593,8 +1838,9 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles) {
 }
 
 bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw) {
-    if (H <= 0 || E % H || (ntw != 1 && ntw != 2)) return false;
+    if (H <= 0 || E % H || ntw < 0 || ntw > 2) return false;
     const int D = E / H;
+    if (ntw == 0) return max_len <= 128 && D == 32 && E == 384 && wtype == W_Q4_0;  // qkv_attention_pc_kernel
     return max_len <= 128 && (D == 32 || D == 64) && H % (192 / (3 * D) * ntw) == 0 && E % KC == 0 &&
            wtype != W_F32;
 }

@@ -177,6 +177,7 @@ struct DevMat {
 struct DevLayer {
     WPtr qkv, o, up, down;
     I8W o8, up8, down8;  // Q4 weights for the int8-MFMA GEMMs (gemm_i8.hip)
+    I8W qkv8;            // head-major QKV on the int8 MFMA (qkva_ntw 0: qkv_attention_pc_kernel + i8 EPI_QKV)
     WPtr qkv_plain;  // head-major QKV in grouped, plain tile order: qkv_attention_kernel's copy (when supported)
     float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
@@ -669,7 +670,12 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
+            qf.Wi = L.qkv8;  // (qkva_ntw 0)
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
+        } else if (ctx->qkva_ntw == 0) {  // the int8 QKV of the producer / consumer kernel, unfused
+            q.Wi = L.qkv8;
+            LAUNCH_OK("gemm_qkv", launch_gemm_i8(wt, EPI_QKV, q, (int)rows, st));
+            LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
         } else {
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
@@ -1023,14 +1029,17 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                     const GGUFTensor *bt = part == 0 ? l.q_b : part == 1 ? l.k_b : l.v_b;
                     bqkv[dst] = ((const float *)bt->data)[src];
                 }
-        if (qkv_attention_supported(ctx->wtype, (int)E, (int)ctx->hp.n_head, 128, ctx->qkva_ntw)) {
+        if (ctx->qkva_ntw == 0) {
+            // producer / consumer kernel and its unfused twin: int8 codes, head-major f-tiles
+            if (!upload_i8(tr, dl.qkv8, wt, rows, E)) return false;
+        } else if (qkv_attention_supported(ctx->wtype, (int)E, (int)ctx->hp.n_head, 128, ctx->qkva_ntw)) {
             // undo repack's column interleave (row 32p + 2c + t <- 32p + 16t + c) so
             // that repacked tile j holds features 16j .. 16j + 15 in order
             // after the grouped tile order (kernels.hip qkv_attention_kernel): tile
             // G tpp q + G w + t <- n-tile w of 192-feature unit G q + t (tpp = 12
             // n-tiles per unit: a head pair at head dim 32, one head at 64; G =
             // units per main loop; G = 1 is the plain order)
-            const size_t tpp = 12, G = (size_t)ctx->qkva_ntw;
+            const size_t tpp = 12, G = (size_t)std::max(1, ctx->qkva_ntw);
             std::vector<const uint8_t *> quad(rows.size()), plain(rows.size());
             for (size_t T = 0; T < rows.size() / 16; T++) {
                 const size_t src = tpp * (G * (T / (G * tpp)) + T % G) + (T % (G * tpp)) / G;
@@ -1051,7 +1060,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                 for (int t = 0; t < 2; t++)
                     for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
         }
-        if (!upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
+        if (ctx->qkva_ntw != 0 && !upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
         // each projection in the one format its GEMM reads (int8 or split fp16)
         if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E))) ||
             !(ctx->i8_up ? upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) : upload_packed(tr, dl.up, repack(wt, up_rows, E))) ||
@@ -1174,8 +1183,8 @@ bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
             return false;
         }
         if (p.first == "qkva_ntw") {
-            if (v != 1 && v != 2) {
-                set_err("bert_amd option qkva_ntw: must be 1 or 2");
+            if (v < 0 || v > 2) {
+                set_err("bert_amd option qkva_ntw: must be 0, 1 or 2");
                 return false;
             }
             ctx->qkva_ntw = (int)v;
@@ -1308,6 +1317,9 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     std::string i8_spec;
     if (!parse_load_options(ctx.get(), opts, i8_spec)) return nullptr;
     i8_select(ctx.get(), i8_spec);
+    // the producer / consumer fused kernel exists for head dim 32 at n_embd 384
+    // (MiniLM); other shapes take the head-pair kernel on the same plain-order copy
+    if (ctx->qkva_ntw == 0 && !qkv_attention_supported(ctx->wtype, (int)E, hp.n_head, 128, 0)) ctx->qkva_ntw = 1;
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {

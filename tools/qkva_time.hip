@@ -76,6 +76,24 @@ int main(int argc, char **argv) {
     g.K = E;
     g.N = 3 * E;
     g.head_dim = D;
+    // the producer / consumer kernel's int8 QKV weights (codes in [-8, 7], fp16 block scales)
+    {
+        std::vector<int8_t> wq((size_t)3 * E * E);
+        uint32_t x = 77;
+        for (auto &v : wq) {
+            x = x * 1664525u + 1013904223u;
+            v = (int8_t)((int)((x >> 24) & 15) - 8);
+        }
+        void *dq;
+        CK(hipMalloc(&dq, wq.size()));
+        CK(hipMemcpy(dq, wq.data(), wq.size(), hipMemcpyHostToDevice));
+        g.Wi.q = (const int8_t *)dq;
+        std::vector<uint16_t> dh((size_t)3 * E * (E / 32), h16(0.01f));
+        void *dd;
+        CK(hipMalloc(&dd, dh.size() * 2));
+        CK(hipMemcpy(dd, dh.data(), dh.size() * 2, hipMemcpyHostToDevice));
+        g.Wi.dh = (const uint16_t *)dd;
+    }
     AttnArgs a{};
     a.offsets = d_off;
     a.E = E;
@@ -102,10 +120,15 @@ int main(int argc, char **argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &d_st, sizeof(d_st)));
     { const int nb = S; CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_nblk), &nb, sizeof(nb))); }
 #endif
+    const bool pc = argc > 2 && !strcmp(argv[2], "pc");  // the producer / consumer kernel
     for (int K : {E, 0}) {
+        if (pc && K == 0) break;
         g.K = K;
         auto launch = [&] {
-            hipLaunchKernelGGL((qkv_attention_kernel<W_Q4_0, 32, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
+            if (pc)
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<false>), dim3(S), dim3(QKPC_NW * 64), 0, 0, g, a);
+            else
+                hipLaunchKernelGGL((qkv_attention_kernel<W_Q4_0, 32, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
         };
         for (int i = 0; i < 3; i++) launch();
         CK(hipGetLastError());
@@ -116,7 +139,7 @@ int main(int argc, char **argv) {
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        printf("qkv_attention q4_0 K=%d: %8.1f us\n", K, ms * 1000.0 / iters);
+        printf("qkv_attention%s q4_0 K=%d: %8.1f us\n", pc ? "_pc" : "", K, ms * 1000.0 / iters);
         fflush(stdout);
 #ifdef PHASE_STAMPS
         if (K == E) {
@@ -125,8 +148,13 @@ int main(int argc, char **argv) {
             CK(hipDeviceSynchronize());
             std::vector<unsigned long long> h(n_st);
             CK(hipMemcpy(h.data(), d_st, n_st * 8, hipMemcpyDeviceToHost));
-            const char *names[] = {"main", "split0", "attn0", "split1", "attn1", "->quad"};
-            stamp_report(h, S, STAMP_TILES, 6, names, ms * 1000.0 / iters);
+            if (pc) {
+                const char *names[] = {"main|attn", "split|store", "->period"};
+                stamp_report(h, S, STAMP_TILES, 3, names, ms * 1000.0 / iters);
+            } else {
+                const char *names[] = {"main", "split0", "attn0", "split1", "attn1", "->quad"};
+                stamp_report(h, S, STAMP_TILES, 6, names, ms * 1000.0 / iters);
+            }
         }
 #endif
     }
