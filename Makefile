@@ -98,3 +98,11 @@ $(BUILD)/phase_stamps: tools/phase_stamps.hip $(SRC)/gemm_i8.hip $(SRC)/kernels.
 $(BUILD)/qkva_stamps: tools/qkva_time.hip tools/stamps.h $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DPHASE_STAMPS=1 $< -o $@
+
+# the long-sentence attention's timing and per-stage stamps (tools/attn_long_time.hip)
+$(BUILD)/attn_long_time: tools/attn_long_time.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) $< -o $@
+$(BUILD)/attn_long_stamps: tools/attn_long_time.hip tools/stamps.h $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i8_core.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DPHASE_STAMPS=1 $< -o $@

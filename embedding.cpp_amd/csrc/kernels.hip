@@ -1717,29 +1717,33 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                     }
                     return S;
                 };
-                // pass 1: max of the unscaled K.Q (x -> fl(x * scale) is monotonic, so
-                // fl(max * scale) is ggml's max of the scaled scores).  Two key tiles at
-                // a time: their MFMA chains are independent, so one covers the
-                // other's latency (a consumer wave is alone in its role on its SIMD)
+                // pass 1: the score tiles (up to 4: n <= 128 keys), kept in registers for
+                // pass 2, and their max — of the unscaled K.Q: x -> fl(x * scale) is
+                // monotonic, so fl(max * scale) is ggml's max of the scaled scores.  The
+                // tiles' MFMA chains are independent, so they cover each other's latency
+                // (a consumer wave is the only one of its role on its SIMD)
+                float16v Sk[4];
                 float mx = -INFINITY;
-                for (int kt = 0; kt < nkt; kt += 2) {
-                    const float16v S = scores(kt);
-                    if (kt + 1 < nkt) {
-                        const float16v S1 = scores(kt + 1);
 #pragma unroll
-                        for (int j = 0; j < 16; j++) mx = fmaxf(mx, S1[j]);
+                for (int kt = 0; kt < 4; kt++) {
+                    if (kt < nkt) {
+                        Sk[kt] = scores(kt);
+#pragma unroll
+                        for (int j = 0; j < 16; j++) mx = fmaxf(mx, Sk[kt][j]);
                     }
-#pragma unroll
-                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
                 }
                 mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
                 const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
-                // pass 2: p = exp_tab[fp16(s - max)], the exact integer sum of p * 2^24, V.P
-                // (key tiles in order into o; two tiles' scores and softmax in flight)
-                auto softmax = [&](const float16v &S, half8 (&ph)[2]) {
+                // pass 2: p = exp_tab[fp16(s - max)], the exact integer sum of p * 2^24, and
+                // V.P over the key tiles in order
+                o[0] = float16v{};
+#pragma unroll
+                for (int kt = 0; kt < 4; kt++) {
+                    if (kt >= nkt) continue;
+                    half8 ph[2];
 #pragma unroll
                     for (int j = 0; j < 16; j += 2) {
-                        const float2v d2 = mx2 - float2v{S[j], S[j + 1]} * sc2;
+                        const float2v d2 = mx2 - float2v{Sk[kt][j], Sk[kt][j + 1]} * sc2;
                         uint16_t pb[2];
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
@@ -1750,20 +1754,7 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                         const float2v pp = float2v{h2f(pb[0]), h2f(pb[1])} * float2v{16777216.0f, 16777216.0f};
                         sum += (uint32_t)pp[0] + (uint32_t)pp[1];
                     }
-                };
-                o[0] = float16v{};
-                for (int kt = 0; kt < nkt; kt += 2) {
-                    const bool two = kt + 1 < nkt;
-                    const float16v S = scores(kt);
-                    float16v S1;
-                    if (two) S1 = scores(kt + 1);
-                    half8 ph[2], ph1[2];
-                    softmax(S, ph);
                     attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph, 0);
-                    if (two) {
-                        softmax(S1, ph1);
-                        attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt + 32, r, hh, ph1, 0);
-                    }
                 }
             }
             STAMP(p, 1, NW);
@@ -1870,11 +1861,19 @@ constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, que
 #define ATTN_LONG_KT_UNROLL(D) 1  // A/B: -D'ATTN_LONG_KT_UNROLL(D)=4' (the round-2 form)
 #endif
 
+// keys per staged chunk, waves per SIMD (the register budget: 4 -> 128 VGPRs)
+#ifndef ATTN_LONG_NK
+#define ATTN_LONG_NK(D) 128
+#endif
+#ifndef ATTN_LONG_OCC
+#define ATTN_LONG_OCC(D) ((D) == 32 ? 4 : 1)
+#endif
+
 template <int WT, int D>
 // D = 32: two workgroups per CU (78 KiB of LDS each; the register budget
 // capped at 128 for four waves per SIMD) — 423 -> 333 us at MiniLM 512 x 256
-__global__ __launch_bounds__(ATTN_LONG_NW * 64, D == 32 ? 4 : 1) void attention_long_kernel(AttnArgs a) {
-    constexpr int NK = 128, KST = D + 8, VST = NK + 4, NT = ATTN_LONG_NW * 64;
+__global__ __launch_bounds__(ATTN_LONG_NW * 64, ATTN_LONG_OCC(D)) void attention_long_kernel(AttnArgs a) {
+    constexpr int NK = ATTN_LONG_NK(D), KST = D + 8, VST = NK + 4, NT = ATTN_LONG_NW * 64;
     __shared__ __attribute__((aligned(16))) _Float16 Kh[NK * KST], Kl[NK * KST], Vh[D * VST], Vl[D * VST];
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
@@ -1976,12 +1975,16 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, D == 32 ? 4 : 1) void attention_
 #pragma unroll
     for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
     fetch(0, false);
+    const int sbid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);  // (phase stamps)
+    (void)sbid;
     for (int st = 0; st < 2 * nch; st++) {
         const bool p2 = st >= nch;
         const int c = p2 ? st - nch : st;
+        STAMPB(sbid, st, 0, ATTN_LONG_NW);
         __syncthreads();  // the previous stage's LDS reads are done
         commit(p2);
         __syncthreads();
+        STAMPB(sbid, st, 1, ATTN_LONG_NW);
         if (st + 1 < 2 * nch) fetch(st + 1 < nch ? st + 1 : st + 1 - nch, st + 1 >= nch);
         if (st == nch) mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;  // pass 1 complete
         if (!active) continue;
@@ -2021,6 +2024,7 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, D == 32 ? 4 : 1) void attention_
                 attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
             }
         }
+        STAMPB(sbid, st, 2, ATTN_LONG_NW);
     }
     double tot = (double)sum * 0x1p-24;  // exact (< 2^34 units), and so is the pair sum
     tot += __shfl_xor(tot, 32);

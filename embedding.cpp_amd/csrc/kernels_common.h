@@ -24,14 +24,16 @@ typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 constexpr int STAMP_TILES = 32;
 static __device__ unsigned long long *g_stamp_buf;  // set by the tool before any launch
 static __device__ int g_stamp_nblk;                 // workgroups the buffer holds
-#define STAMP(it, slot, nw)                                                                                     \
+#define STAMPB(bid, it, slot, nw)                                                                               \
     do {                                                                                                        \
         const int w_ = threadIdx.x >> 6;                                                                        \
         if ((threadIdx.x & 63) == 0 && (w_ == 0 || w_ == (nw) - 1) && (it) < STAMP_TILES && g_stamp_buf &&      \
-            (int)blockIdx.x < g_stamp_nblk)                                                                     \
-            g_stamp_buf[((blockIdx.x * STAMP_TILES + (it)) * 2 + (w_ != 0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+            (int)(bid) < g_stamp_nblk)                                                                          \
+            g_stamp_buf[(((bid) * STAMP_TILES + (it)) * 2 + (w_ != 0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#define STAMP(it, slot, nw) STAMPB(blockIdx.x, it, slot, nw)
 #else
+#define STAMPB(bid, it, slot, nw) ((void)0)
 #define STAMP(it, slot, nw) ((void)0)
 #endif
 

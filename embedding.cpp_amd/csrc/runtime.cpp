@@ -258,9 +258,12 @@ struct bert_ctx {
     std::vector<std::unique_ptr<Replica>> reps;
     // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
     bool i8_o = false, i8_up = false, i8_down = false;
-    // 192-feature units per main loop of the fused QKV + attention kernel (1 or
-    // 2): the tile grouping of its QKV weight copy, fixed at load
-    int qkva_ntw = 2;
+    // the fused QKV + attention kernel's form, fixed at load: 1 or 2 = the
+    // head-pair kernel with that many 192-feature units per main loop (the tile
+    // grouping of its QKV weight copy), 0 = the producer / consumer kernel on an
+    // int8 head-major copy (Q4_0, head dim 32, n_embd 384); -1 (default) = 0
+    // where it exists, else 2
+    int qkva_ntw = -1;
     // run_pipeline knobs: defaults, then the load options (LoadOpts), then
     // bert_amd_set_option; nothing is read from the environment after load.
     // unfused: every batch on the QKV GEMM + attention pair (A/B checks);
@@ -1183,8 +1186,8 @@ bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
             return false;
         }
         if (p.first == "qkva_ntw") {
-            if (v < 0 || v > 2) {
-                set_err("bert_amd option qkva_ntw: must be 0, 1 or 2");
+            if (v < -1 || v > 2) {
+                set_err("bert_amd option qkva_ntw: must be -1 (auto), 0, 1 or 2");
                 return false;
             }
             ctx->qkva_ntw = (int)v;
@@ -1317,9 +1320,14 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     std::string i8_spec;
     if (!parse_load_options(ctx.get(), opts, i8_spec)) return nullptr;
     i8_select(ctx.get(), i8_spec);
-    // the producer / consumer fused kernel exists for head dim 32 at n_embd 384
-    // (MiniLM); other shapes take the head-pair kernel on the same plain-order copy
-    if (ctx->qkva_ntw == 0 && !qkv_attention_supported(ctx->wtype, (int)E, hp.n_head, 128, 0)) ctx->qkva_ntw = 1;
+    // the producer / consumer fused kernel exists for Q4_0 at head dim 32, n_embd
+    // 384 (MiniLM; measured +1.2% batch-1024, +6% ragged over the head-pair
+    // kernel): auto takes it there and the 2-unit head-pair kernel
+    // elsewhere; an explicit 0 on another shape takes the head-pair kernel on
+    // the same plain-order copy
+    const bool pc_ok = qkv_attention_supported(ctx->wtype, (int)E, hp.n_head, 128, 0);
+    if (ctx->qkva_ntw < 0) ctx->qkva_ntw = pc_ok ? 0 : 2;
+    if (ctx->qkva_ntw == 0 && !pc_ok) ctx->qkva_ntw = 1;
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {

@@ -36,8 +36,10 @@ BERT_API struct bert_ctx *bert_amd_load(const char *fname, const int32_t *device
      "i8"       Q4 projections on the int8-MFMA GEMMs: "0" none, "all", or a
                 list of up, o, down joined by '+' (default: up+down at n_embd
                 384, up otherwise)
-     "qkva_ntw" 1 | 2   head-pair units per main loop of the fused QKV +
-                attention kernel (default 2)
+     "qkva_ntw" the fused QKV + attention kernel: 0 producer / consumer
+                waves on an int8 QKV copy (Q4_0, head dim 32, n_embd 384;
+                elsewhere 1), 1 | 2 head-pair units per main loop of the
+                head-pair kernel, -1 (default) 0 where it exists, else 2
    and every bert_amd_set_option key below.  Returns NULL on error (an unknown
    key or a bad value included). */
 BERT_API struct bert_ctx *bert_amd_load_opts(const char *fname, const int32_t *devices, int32_t n_devices,

@@ -675,29 +675,32 @@ def test_encode_batch_lanes_bitwise(model_dir):
 
 
 def test_producer_consumer_kernel(model_dir):
-    """qkv_attention_pc_kernel (load option qkva_ntw=0, Q4_0 MiniLM: producer
-    waves run head h's QKV projection on the int8 MFMA while consumer waves
-    run head h - 1's attention): the golden fixtures within the bound; its
-    unfused twin (i8 EPI_QKV GEMM + attention, small batches and sentences over
-    128 tokens) bitwise equal to it; packed short sentences bitwise equal to
-    the sentence alone; and within the north-star bar of the head-quad kernel."""
+    """qkv_attention_pc_kernel (load option qkva_ntw=0, the default for Q4_0
+    MiniLM: producer waves run head h's QKV projection on the int8 MFMA while
+    consumer waves run head h - 1's attention): the golden fixtures within the
+    bound; its unfused twin (i8 EPI_QKV GEMM + attention, small batches and
+    sentences over 128 tokens) bitwise equal to it; packed short sentences
+    bitwise equal to the sentence alone; and within the north-star bar of the
+    head-quad kernel (qkva_ntw=2), which stays covered here on Q4_0 too."""
     import oracle
-    p, m = get_model(model_dir, "minilm", "q4_0")
+    p, _ = get_model(model_dir, "minilm", "q4_0")
     m0 = bertlib.BertModel(p, options={"qkva_ntw": 0})
+    m2 = bertlib.BertModel(p, options={"qkva_ntw": 2})
     try:
         for case in ("c3_minilm_q4_0", "c3_minilm_q4_0_ragged", "minilm_q4_0_std01"):
             meta, toks, want = load_case(case)
             pm = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-            mm = m0 if pm == p else bertlib.BertModel(pm, options={"qkva_ntw": 0})
-            try:
-                mm.set_option("fuse_min", 0)
-                c = cos(mm.eval_batch(toks), want)
-                print(f"pc {case}: 1-cos max {1 - c.min():.2e}")
-                assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
-            finally:
-                mm.set_option("fuse_min", 48)
-                if mm is not m0:
-                    mm.close()
+            for ntw, base in ((0, m0), (2, m2)):
+                mm = base if pm == p else bertlib.BertModel(pm, options={"qkva_ntw": ntw})
+                try:
+                    mm.set_option("fuse_min", 0)
+                    c = cos(mm.eval_batch(toks), want)
+                    print(f"qkva_ntw {ntw} {case}: 1-cos max {1 - c.min():.2e}")
+                    assert np.all(1 - c <= parity_bound(meta)), (case, ntw, 1 - c)
+                finally:
+                    mm.set_option("fuse_min", 48)
+                    if mm is not base:
+                        mm.close()
         rng = np.random.default_rng(123)
         batches = [[sentence(800 + i, 128, 30522) for i in range(64)],
                    [[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in rng.integers(2, 129, 300)],
@@ -711,8 +714,9 @@ def test_producer_consumer_kernel(model_dir):
             m0.set_option("fuse_min", 48)
             bad = [i for i in range(len(toks)) if not np.array_equal(fused[i], unfused[i])]
             assert not bad, (bad[:10], [len(toks[i]) for i in bad[:10]])
-            assert cos(fused, m.eval_batch(toks)).min() >= COS_TOL
+            assert cos(fused, m2.eval_batch(toks)).min() >= COS_TOL
         sub = batches[1][:8]
         assert cos(m0.eval_batch(sub), oracle.Oracle(p).eval_batch(sub, 0)).min() >= COS_TOL
     finally:
         m0.close()
+        m2.close()
