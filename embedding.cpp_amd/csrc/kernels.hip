@@ -369,6 +369,34 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__r
     ln_rows16<WT, NBLK, 256>(X, lnw, lnb, eps, out, (int64_t)blockIdx.x * 16, red, stat);
 }
 
+// The LayerNorm of a residual GEMM's row tile, by the workgroup that wrote its
+// last column tile (GemmArgs::ln_cnt): every workgroup releases its X stores
+// (device-scope fence: the column tiles of a row tile may sit on different
+// XCDs, whose L2s are not coherent) and counts itself in; the last one
+// acquires, resets the counter for the next launch and runs ln_rows16 over
+// the tile's 16-row slices — the separate ln_rows_kernel's code, so the bits
+// are the same.  smem: >= 16 * (N / 32) doubles + 16 floats, free after the
+// main loop.
+template <int WT, int NT, int BM>
+__device__ __forceinline__ void ln_tile_finish(const GemmArgs &args, char *smem, int mt, int n_ntiles, int64_t m0) {
+    __shared__ int last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(args.ln_cnt + mt, 1) == n_ntiles - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (threadIdx.x == 0) args.ln_cnt[mt] = 0;
+    double *red = (double *)smem;
+    float *stat = (float *)(smem + 16 * 32 * sizeof(double));
+    for (int sl = 0; sl < BM / 16; sl++) {
+        switch (args.N) {  // (the host enables this for 768 and 1024 only)
+            case 768: ln_rows16<WT, 24, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, m0 + 16 * sl, red, stat); break;
+            default: ln_rows16<WT, 32, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, m0 + 16 * sl, red, stat); break;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // GEMM: C[M][N] = A[M][K] . W[N][K]^T on MFMA, fused epilogues.
 //
@@ -880,6 +908,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         if (t == 1234.5678f) args.X[tid] = t;
     } else if constexpr (EPI == EPI_RESID) {  // X = (b + W.x) + X, in registers
         resid_epilogue<RT, NP>(args, m0, colw, acc);
+        if (args.ln_cnt) ln_tile_finish<WT, NT, BM>(args, smem, (int)(m0 / BM), n_ntiles, m0);
     } else if constexpr (EPI == EPI_QKV) {
         // y = b + W.x in f32 (ggml), split hi = fp16(y), lo = fp16(y - hi) for the
         // attention MFMAs.  A column pair lies wholly in Q|K or in V (E % 32 == 0).
@@ -1561,6 +1590,9 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 // tiles; the tiles hold the next head).  LDS: the panel (58 KB), one head's
 // tiles (57 KB), the exp table (40 KB).
 constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
+#ifndef QKPC_CPRIO
+#define QKPC_CPRIO 0  // static issue priority of the consumer waves (A/B)
+#endif
 
 template <bool PK>
 __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
@@ -1677,6 +1709,9 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         }
     } else {
         // ---- consumer: query block qb of head p - 1 (32 queries of one sentence)
+#if QKPC_CPRIO > 0
+        __builtin_amdgcn_s_setprio(QKPC_CPRIO);
+#endif
         const int qb = wv - NP;
         int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
         asm volatile("" : "+v"(lim));
@@ -1868,6 +1903,9 @@ constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, que
 #ifndef ATTN_LONG_OCC
 #define ATTN_LONG_OCC(D) ((D) == 32 ? 4 : 1)
 #endif
+#ifndef ATTN_LONG_PRIO
+#define ATTN_LONG_PRIO 0  // A/B: issue priority 1 for waves NW/2 .. NW - 1
+#endif
 
 template <int WT, int D>
 // D = 32: two workgroups per CU (78 KiB of LDS each; the register budget
@@ -1972,40 +2010,63 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, ATTN_LONG_OCC(D)) void attention
     float mx = -INFINITY;
     uint64_t sum = 0;  // the probabilities' exact sum in units of 2^-24 (as in attention_short_kernel)
     float16v o[D / 32];
-#pragma unroll
-    for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
-    fetch(0, false);
     const int sbid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);  // (phase stamps)
     (void)sbid;
-    for (int st = 0; st < 2 * nch; st++) {
-        const bool p2 = st >= nch;
-        const int c = p2 ? st - nch : st;
+#if ATTN_LONG_PRIO
+    if (wv >= ATTN_LONG_NW / 2) __builtin_amdgcn_s_setprio(1);  // the later-dispatched half of each SIMD pair
+#endif
+    // stage st: the staged chunk (pass 1: K of chunk st; pass 2: K and V^T of
+    // chunk st - nch) goes from registers to LDS, and the next stage's loads start
+    auto stage = [&](int st) {
         STAMPB(sbid, st, 0, ATTN_LONG_NW);
         __syncthreads();  // the previous stage's LDS reads are done
-        commit(p2);
+        commit(st >= nch);
         __syncthreads();
         STAMPB(sbid, st, 1, ATTN_LONG_NW);
         if (st + 1 < 2 * nch) fetch(st + 1 < nch ? st + 1 : st + 1 - nch, st + 1 >= nch);
-        if (st == nch) mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;  // pass 1 complete
-        if (!active) continue;
-        // the key-tile loop stays rolled — unrolled, the compiler keeps more
-        // tiles' operands live: at D = 64 it spilled 80 B/lane at 256 VGPRs
-        // (208 VGPRs, no scratch rolled); at D = 32 rolled is what fits the
-        // 128-VGPR budget of two workgroups per CU (20 B/lane of scratch)
-        // (Software-pipelining the score tiles — the next tile's K.Q MFMAs issued
-        // before this tile's softmax — measured 1 - 3 % slower: not kept.)
-        constexpr int KTU = ATTN_LONG_KT_UNROLL(D);
-#pragma unroll KTU
-        for (int kt = 0; kt < NK / 32; kt++) {
-            const int k0 = c * NK + 32 * kt;
-            if (k0 >= n) continue;
-            float16v S = scores(k0, 32 * kt);
-            if (!p2) {  // pass 1: maxima
+    };
+    fetch(0, false);
+    // pass 1: maxima.  Two key tiles at a time (independent MFMA chains; o is not live yet)
+    for (int c = 0; c < nch; c++) {
+        stage(c);
+        if (active) {
 #pragma unroll
-                for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
-            } else {    // pass 2: p, sum, P.V
+            for (int kt = 0; kt < NK / 32; kt += 2) {
+                const int k0 = c * NK + 32 * kt;
+                if (k0 >= n) break;
+                const float16v S0 = scores(k0, 32 * kt);
+                if (k0 + 32 < n) {
+                    const float16v S1 = scores(k0 + 32, 32 * kt + 32);
+#pragma unroll
+                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, fmaxf(S0[j], S1[j]));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 16; j++) mx = fmaxf(mx, S0[j]);
+                }
+            }
+        }
+        STAMPB(sbid, c, 2, ATTN_LONG_NW);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; dt++) o[dt] = float16v{};
+    // pass 2: p, sum, P.V.  The key-tile loop stays rolled — unrolled, the
+    // compiler keeps more tiles' operands live: at D = 64 it spilled 80 B/lane
+    // at 256 VGPRs (208 VGPRs, no scratch rolled); at D = 32 rolled is what fits
+    // the 128-VGPR budget of two workgroups per CU.  (Software-pipelining the
+    // score tiles — the next tile's K.Q MFMAs issued before this tile's softmax
+    // — measured 1 - 3 % slower: not kept.)
+    const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
+    for (int c = 0; c < nch; c++) {
+        stage(nch + c);
+        if (active) {
+            constexpr int KTU = ATTN_LONG_KT_UNROLL(D);
+#pragma unroll KTU
+            for (int kt = 0; kt < NK / 32; kt++) {
+                const int k0 = c * NK + 32 * kt;
+                if (k0 >= n) break;
+                float16v S = scores(k0, 32 * kt);
                 uint32_t part = 0;  // 16 terms <= 2^24
-                const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
 #pragma unroll
                 for (int j = 0; j < 16; j += 2) {
                     // |s - max| as fp16 (s scaled); masked -inf -> +inf -> 0.  Two scores
@@ -2013,8 +2074,7 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, ATTN_LONG_OCC(D)) void attention
                     const float2v d2 = mx2 - float2v{S[j], S[j + 1]} * sc2;
 #pragma unroll
                     for (int e = 0; e < 2; e++) {
-                        const float de = d2[e];
-                        const uint32_t hm = f2h(de);
+                        const uint32_t hm = f2h(d2[e]);
                         S[j + e] = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
                     }
                     const float2v p2 = float2v{S[j], S[j + 1]} * float2v{16777216.0f, 16777216.0f};
@@ -2024,7 +2084,7 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, ATTN_LONG_OCC(D)) void attention
                 attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S);
             }
         }
-        STAMPB(sbid, st, 2, ATTN_LONG_NW);
+        STAMPB(sbid, nch + c, 2, ATTN_LONG_NW);
     }
     double tot = (double)sum * 0x1p-24;  // exact (< 2^34 units), and so is the pair sum
     tot += __shfl_xor(tot, 32);
