@@ -113,11 +113,6 @@ struct GemmArgs {
     const float *ln_w = nullptr, *ln_b = nullptr;
     float eps = 0.f;
     HalfTable gelu;                      // EPI_GELU_ACT: ggml's fp16 GELU table
-    // EPI_RESID with N = 768 / 1024 only: per 128-row tile counters (zero
-    // between launches; null = no LayerNorm).  The workgroup that finishes a row
-    // tile's last column tile normalises the tile's rows in place (ln_w, ln_b,
-    // eps) and writes out_act: the separate ln pass fused into the GEMM.
-    int *ln_cnt = nullptr;
 };
 
 struct EmbedArgs {

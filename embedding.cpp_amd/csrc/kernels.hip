@@ -296,12 +296,12 @@ __device__ __forceinline__ void ln_rows16(float *X, const float *__restrict__ ln
         const int t = tid + NT * it, qq = t & 3, b = (t >> 2) % NBLK, r = (t >> 2) / NBLK, c = 32 * b + 8 * qq;
         const float4v *xp = (const float4v *)(X + (row0 + r) * (int64_t)E + c);
         const float4v x0 = xp[0], x1 = xp[1];
-        double s = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             v[it][j] = x0[j];
             v[it][4 + j] = x1[j];
         }
+        double s = 0.0;
 #pragma unroll
         for (int j = 0; j < 8; j++) s += (double)v[it][j];
         s += __shfl_xor(s, 1);
@@ -367,34 +367,6 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float *X, const float *__r
     __shared__ double red[16 * NBLK];
     __shared__ float stat[16];
     ln_rows16<WT, NBLK, 256>(X, lnw, lnb, eps, out, (int64_t)blockIdx.x * 16, red, stat);
-}
-
-// The LayerNorm of a residual GEMM's row tile, by the workgroup that wrote its
-// last column tile (GemmArgs::ln_cnt): every workgroup releases its X stores
-// (device-scope fence: the column tiles of a row tile may sit on different
-// XCDs, whose L2s are not coherent) and counts itself in; the last one
-// acquires, resets the counter for the next launch and runs ln_rows16 over
-// the tile's 16-row slices — the separate ln_rows_kernel's code, so the bits
-// are the same.  smem: >= 16 * (N / 32) doubles + 16 floats, free after the
-// main loop.
-template <int WT, int NT, int BM>
-__device__ __forceinline__ void ln_tile_finish(const GemmArgs &args, char *smem, int mt, int n_ntiles, int64_t m0) {
-    __shared__ int last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(args.ln_cnt + mt, 1) == n_ntiles - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    if (threadIdx.x == 0) args.ln_cnt[mt] = 0;
-    double *red = (double *)smem;
-    float *stat = (float *)(smem + 16 * 32 * sizeof(double));
-    for (int sl = 0; sl < BM / 16; sl++) {
-        switch (args.N) {  // (the host enables this for 768 and 1024 only)
-            case 768: ln_rows16<WT, 24, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, m0 + 16 * sl, red, stat); break;
-            default: ln_rows16<WT, 32, NT>(args.X, args.ln_w, args.ln_b, args.eps, args.out_act, m0 + 16 * sl, red, stat); break;
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -908,7 +880,6 @@ __global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs args, int n_mtil
         if (t == 1234.5678f) args.X[tid] = t;
     } else if constexpr (EPI == EPI_RESID) {  // X = (b + W.x) + X, in registers
         resid_epilogue<RT, NP>(args, m0, colw, acc);
-        if (args.ln_cnt) ln_tile_finish<WT, NT, BM>(args, smem, (int)(m0 / BM), n_ntiles, m0);
     } else if constexpr (EPI == EPI_QKV) {
         // y = b + W.x in f32 (ggml), split hi = fp16(y), lo = fp16(y - hi) for the
         // attention MFMAs.  A column pair lies wholly in Q|K or in V (E % 32 == 0).
@@ -1593,6 +1564,9 @@ constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
 #ifndef QKPC_CPRIO
 #define QKPC_CPRIO 0  // static issue priority of the consumer waves (A/B)
 #endif
+#ifndef QKPC_DEFER
+#define QKPC_DEFER 0  // consumers store head h's context during head h + 1's period (A/B)
+#endif
 
 template <bool PK>
 __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
@@ -1716,20 +1690,33 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
         asm volatile("" : "+v"(lim));
         const _Float16 *Qh = plane(0), *Ql = plane(1), *Kh = plane(2), *Kl = plane(3), *Vh = plane(4), *Vl = plane(5);
+        int kb = 0, len = n, qrel = 32 * qb, vs = 0;
+        if constexpr (PK) {
+            kb = qtab[qb][0];
+            len = qtab[qb][1];
+            qrel = qtab[qb][2];
+            vs = qtab[qb][3];
+        }
+        const bool qact = PK ? len > 0 : qrel < n;
+        const int qrow = kb + qrel + r;  // tile row of this lane's query (rows past the sentence
+                                         // read finite LDS data; never stored)
+        float16v o[1];
+        uint32_t sum = 0;
+        // the context of head h, o * (1 / sum) in the O-projection's format
+        auto store_ctx = [&](int h) {
+            sum += __shfl_xor(sum, 32);
+            int orow = qrow;
+            asm volatile("" : "+v"(orow));
+            attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, h, hh, 0);
+        };
         for (int p = 0; p <= H; p++) {
             const int head = p - 1;
-            int kb = 0, len = n, qrel = 32 * qb, vs = 0;
-            if constexpr (PK) {
-                kb = qtab[qb][0];
-                len = qtab[qb][1];
-                qrel = qtab[qb][2];
-                vs = qtab[qb][3];
-            }
-            const bool act = head >= 0 && (PK ? len > 0 : qrel < n);
-            const int qrow = kb + qrel + r;  // tile row of this lane's query (rows past the sentence
-                                             // read finite LDS data; never stored)
-            float16v o[1];
-            uint32_t sum = 0;
+            const bool act = head >= 0 && qact;
+#if QKPC_DEFER
+            // head p - 2's context leaves now, beside the producers' main loop
+            if (act && head >= 1) store_ctx(head - 1);
+#endif
+            sum = 0;
             if (act) {
                 const int nkt = (len + 31) >> 5;
                 int klim = lim;  // key 32 kt + (j & 3) + 8 (j >> 2) + 4 hh valid while < len
@@ -1794,17 +1781,16 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
             }
             STAMP(p, 1, NW);
             __syncthreads();  // X: this head's tiles may be overwritten
-            if (act) {
-                sum += __shfl_xor(sum, 32);
-                int orow = qrow;
-                asm volatile("" : "+v"(orow));
-                attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, head,
-                                         hh, 0);
-            }
+#if !QKPC_DEFER
+            if (act) store_ctx(head);
+#endif
             STAMP(p, 2, NW);
             __syncthreads();  // Y
             STAMP(p + 1, 0, NW);
         }
+#if QKPC_DEFER
+        if (qact && H >= 1) store_ctx(H - 1);
+#endif
     }
 }
 
@@ -1896,12 +1882,15 @@ constexpr int ATTN_LONG_NW = 8, ATTN_LONG_QB = 32 * ATTN_LONG_NW;  // waves, que
 #define ATTN_LONG_KT_UNROLL(D) 1  // A/B: -D'ATTN_LONG_KT_UNROLL(D)=4' (the round-2 form)
 #endif
 
-// keys per staged chunk, waves per SIMD (the register budget: 4 -> 128 VGPRs)
+// keys per staged chunk, waves per SIMD (the register budget: 4 -> 128 VGPRs).
+// Head dim 64 stages 64-key chunks (77 KiB of LDS) so that two workgroups share
+// a CU, four waves per SIMD (round 4: C5 attention 1531 -> 1383 us, C4 715 ->
+// 674 us at 128 VGPRs, 24-28 B/lane of scratch outside the key-tile loop)
 #ifndef ATTN_LONG_NK
-#define ATTN_LONG_NK(D) 128
+#define ATTN_LONG_NK(D) ((D) == 64 ? 64 : 128)
 #endif
 #ifndef ATTN_LONG_OCC
-#define ATTN_LONG_OCC(D) ((D) == 32 ? 4 : 1)
+#define ATTN_LONG_OCC(D) 4
 #endif
 #ifndef ATTN_LONG_PRIO
 #define ATTN_LONG_PRIO 0  // A/B: issue priority 1 for waves NW/2 .. NW - 1

@@ -192,7 +192,6 @@ struct Workspace {
     int32_t *tok = nullptr, *off = nullptr, *rowpos = nullptr;
     int32_t *tiles = nullptr;  // qkv_attention_kernel's sentence tiles: [first, count] pairs
     int32_t *perm = nullptr;   // eval_device in tile order: caller's index of each sentence
-    int32_t *ln_cnt = nullptr; // per 128-row tile: the residual GEMMs' LayerNorm counters (GemmArgs::ln_cnt), zero between launches
     std::vector<int32_t> h_tiles;
     std::vector<void *> allocs;
     // pinned host staging for the host-pointer ABI
@@ -275,9 +274,6 @@ struct bert_ctx {
     // pair, whose GEMM and attention spread a sentence over many workgroups
     int split = 1, pack = -1, fuse_min = 48;
     bool unfused = false;
-    // residual GEMMs of rows wider than one LN tile (Q4 at n_embd 768 / 1024):
-    // 0 = the LayerNorm in the GEMM (ln_tile_finish), 1 = the separate ln pass (A/B)
-    bool ln_pass = false;
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
     // merging only up to encode_merge_rows sentences (slices that large already
@@ -523,7 +519,7 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
     w.X = w.out = nullptr;
     w.qk_hi = w.qk_lo = w.vt_hi = w.vt_lo = nullptr;
     w.Xa = w.Ca = w.Ua = ActPtr{};
-    w.tok = w.off = w.rowpos = w.tiles = w.perm = w.ln_cnt = nullptr;
+    w.tok = w.off = w.rowpos = w.tiles = w.perm = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const int at = ctx->wtype;
     if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
@@ -533,7 +529,7 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
         !alloc_act(w.allocs, w.Ua, at, rows, I, st) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
         !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4) ||
         !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4) || !dmalloc(w.allocs, &w.tiles, (size_t)seqs * 2 * 4) ||
-        !dmalloc(w.allocs, &w.perm, (size_t)seqs * 4) || !dmalloc(w.allocs, &w.ln_cnt, (size_t)(rows / 128 + 1) * 4))
+        !dmalloc(w.allocs, &w.perm, (size_t)seqs * 4))
         return false;
     // padding rows must hold finite values: zero everything once
     HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, st));
@@ -541,7 +537,6 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
     HIP_OK(hipMemsetAsync(w.qk_lo, 0, (size_t)rows * 2 * E * 2, st));
     HIP_OK(hipMemsetAsync(w.vt_hi, 0, (size_t)rows * E * 2, st));
     HIP_OK(hipMemsetAsync(w.vt_lo, 0, (size_t)rows * E * 2, st));
-    HIP_OK(hipMemsetAsync(w.ln_cnt, 0, (size_t)(rows / 128 + 1) * 4, st));
     w.cap_rows = rows;
     w.cap_seqs = seqs;
     return true;
@@ -709,9 +704,6 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             }
         } else if (ln_fused) {
             LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_LN, 0, o, (int)rows, st));
-        } else if (!ctx->ln_pass && (E == 768 || E == 1024)) {  // the LayerNorm in the GEMM (row tiles of 128)
-            o.ln_cnt = w.ln_cnt + row0 / 128;
-            LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_o_ln", launch_gemm(wt, EPI_RESID, 0, o, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
@@ -755,9 +747,6 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             }
         } else if (ln_fused) {
             LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_LN, 0, dn, (int)rows, st));
-        } else if (!ctx->ln_pass && (E == 768 || E == 1024)) {
-            dn.ln_cnt = w.ln_cnt + row0 / 128;
-            LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_down_ln", launch_gemm(wt, EPI_RESID, 0, dn, (int)rows, st));
             LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
@@ -1148,8 +1137,6 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         ctx->fuse_min = value;
     } else if (k == "unfused") {
         ctx->unfused = value != 0;
-    } else if (k == "ln_pass") {
-        ctx->ln_pass = value != 0;
     } else if (k == "encode_lanes" || k == "encode_merge" || k == "encode_merge_rows") {
         if (need(value >= 1, "must be >= 1")) return -2;
         (k == "encode_lanes" ? ctx->encode_lanes : k == "encode_merge" ? ctx->encode_merge : ctx->encode_merge_rows) = value;
@@ -1167,7 +1154,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // fused kernel's weight grouping); every bert_amd_set_option key is accepted
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
-    static const char *keys[] = {"i8", "qkva_ntw", "split", "pack", "fuse_min", "unfused", "ln_pass",
+    static const char *keys[] = {"i8", "qkva_ntw", "split", "pack", "fuse_min", "unfused",
                                  "encode_lanes", "encode_merge", "encode_merge_rows"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {

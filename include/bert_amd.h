@@ -123,9 +123,6 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
                         kernel (lower latency for small batches)
      "unfused" 0 | 1    1: every batch on the QKV GEMM + attention pair (A/B
                         checks; default 0)
-     "ln_pass" 0 | 1    Q4 at n_embd 768 / 1024: 1 = LayerNorm after the
-                        residual GEMMs in a separate pass (A/B checks); 0
-                        (default) = in the GEMM's last workgroup per row tile
      "encode_lanes" n >= 1 bert_encode_batch: lanes per device, each a host
                         thread with its own workspace and streams (default 2;
                         BERT_AMD_ENCODE_LANES)

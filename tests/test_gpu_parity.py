@@ -721,25 +721,3 @@ def test_producer_consumer_kernel(model_dir):
         m0.close()
         m2.close()
 
-
-def test_ln_in_residual_gemm_bitwise_ln_pass(model_dir):
-    """Q4 rows wider than one LN tile (bge-large Q4_1, n_embd 1024): the residual
-    GEMMs normalise each 128-row tile in the workgroup that writes its last
-    column tile (kernels.hip ln_tile_finish: device-scope fence + counter), with
-    the separate ln pass's code.  Bitwise equal to the separate pass (option
-    ln_pass=1) on long, short and ragged sentences, twice in a row (the counters
-    reset themselves), and the 2-layer golden fixtures within their bound."""
-    meta, toks, want = load_case("c5_bge_q4_1_l2")
-    p, m = get_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    rng = np.random.default_rng(5)
-    batch = toks + [[101] + rng.integers(1000, 30000, int(n) - 2).tolist() + [102] for n in (3, 64, 129, 300, 511, 40)]
-    try:
-        got = m.eval_batch(batch)
-        again = m.eval_batch(batch)
-        m.set_option("ln_pass", 1)
-        ref = m.eval_batch(batch)
-    finally:
-        m.set_option("ln_pass", 0)
-    assert np.array_equal(got, ref) and np.array_equal(again, ref)
-    c = cos(got[:len(toks)], want)
-    assert np.all(1 - c <= parity_bound(meta)), 1 - c

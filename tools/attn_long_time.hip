@@ -111,7 +111,7 @@ static void run(int S, int L, int E, int H, int iters) {
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> h(n_st);
     CK(hipMemcpy(h.data(), d_st, n_st * 8, hipMemcpyDeviceToHost));
-    const int nch = (L + 127) / 128;
+    const int nch = (L + ATTN_LONG_NK(64) - 1) / ATTN_LONG_NK(64);
     // per stage: medians over workgroups
     for (int w = 0; w < 2; w++) {
         printf("  wave %s:", w ? "last" : "0   ");
