@@ -167,32 +167,34 @@ def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
     }.get(name, 0.0) if L else 0.0
 
 
-def pmc_traffic(csv_path: str, kernel_substr: str):
+def pmc_traffic(csv_path: str, kernel_substr):
     """Average corrected HBM bytes per dispatch of one kernel from a rocprofv3
     --pmc FETCH_SIZE / WRITE_SIZE counter CSV (gfx950: FETCH_SIZE counts half the
     bytes of a wide coalesced read — MI355X_MICROARCH.md §HBM — so it is doubled;
-    both counters are in KB)."""
+    both counters are in KB).  kernel_substr: a symbol fragment, or a list of
+    them of which the first that occurs in the CSV is used."""
     import csv
-    vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
-    paths = csv_path.split(",")
-    for p in paths:
-        if not os.path.exists(p):
-            continue
-        with open(p) as f:
-            for row in csv.DictReader(f):
-                name = row.get("Kernel_Name", "")
-                cn = row.get("Counter_Name", "")
-                if kernel_substr in name and cn in vals:
-                    vals[cn].append(float(row.get("Counter_Value", 0)))
-    if not vals["FETCH_SIZE"] or not vals["WRITE_SIZE"]:
-        return None
-    return (2.0 * np.mean(vals["FETCH_SIZE"]) + np.mean(vals["WRITE_SIZE"])) * 1024.0
+    frags = [kernel_substr] if isinstance(kernel_substr, str) else list(kernel_substr)
+    rows = []
+    for p in csv_path.split(","):
+        if os.path.exists(p):
+            with open(p) as f:
+                rows += [(r.get("Kernel_Name", ""), r.get("Counter_Name", ""), r.get("Counter_Value", 0))
+                         for r in csv.DictReader(f)]
+    for frag in frags:
+        vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+        for name, cn, v in rows:
+            if frag in name and cn in vals:
+                vals[cn].append(float(v))
+        if vals["FETCH_SIZE"] and vals["WRITE_SIZE"]:
+            return (2.0 * np.mean(vals["FETCH_SIZE"]) + np.mean(vals["WRITE_SIZE"])) * 1024.0
+    return None
 
 
 # name fragments of the dominant kernels' mangled symbols (for PMC CSV lookup)
 KERNEL_SYMBOL = {
     "gemm_qkv": "gemm_kernel<2, 0,", "gemm_o_ln": "gemm_kernel<2, 2,", "gemm_up_gelu": "i8_up_gelu_kernel",
-    "gemm_down_ln": "i8_ln384_kernel", "attention": "attention_short_kernel", "qkv_attention": "qkv_attention_kernel", "embed_ln": "embed_ln_kernel",
+    "gemm_down_ln": "i8_ln384_kernel", "attention": "attention_short_kernel", "qkv_attention": ["qkv_attention_pc_kernel", "qkv_attention_kernel"], "embed_ln": "embed_ln_kernel",
     "pool_l2": "pool_l2_kernel",
 }
 

@@ -14,7 +14,7 @@ from hbm_summary import load  # noqa: E402
 
 # bench.py kernel names -> fragments of the mangled kernel symbols
 NAMES = {
-    "qkv_attention": ["qkv_attention_kernel"],
+    "qkv_attention": ["qkv_attention_pc_kernel", "qkv_attention_kernel"],
     "gemm_up_gelu": ["i8_up_gelu_kernel", "q4r_up_gelu_kernel", "gemm_kernelILi2ELi1", "gemm_kernel<2, 1,"],
     # default C3 build: o-proj on the split-fp16 LN GEMM, down on the int8 one
     "gemm_o_ln": ["gemm_kernelILi2ELi2", "gemm_kernel<2, 2,", "i8_ln384_kernel"],
