@@ -1,1 +1,1 @@
-cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && bash tools/gpu_r4_final.sh
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && bash tools/gpu_r4_final2.sh
