@@ -359,33 +359,29 @@ namespace bertamd {
 // something else (qkv_attention_pc_kernel).  Weight fragments stream through
 // the same 4-slot register ring as i8_mainloop, two blocks ahead, the weight
 // scales one chunk ahead; the block step is i8_block, so the sums are the
-// chunk-staged main loop's, bit for bit.
-template <int WT, int BM, int F, int T>
-__device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
-                                                     float16v (&acc)[F][T]) {
-    constexpr bool Q1 = WT == W_Q4_1;
-    using C = I8Chunk<BM, Q1>;
-    const int lane = threadIdx.x & 63, hh = lane >> 5;
-    const int nkb = g.K >> 5, nch = g.K / I8_KC;
-    const float4v z4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < F; f++)
-#pragma unroll
-        for (int t = 0; t < T; t++) acc[f][t] = float16v{};
+// chunk-staged main loop's, bit for bit.  The ring lives in the caller
+// (I8ResRing) and runs across calls: ring.start(g, ft) loads f-tile ft's first
+// two blocks and scales; each call consumes the ring for ft0 and, when ftn >= 0,
+// refills it with f-tile ftn's first blocks and scales at its end, so their
+// L2 latency passes during whatever the caller does between two calls.
+template <int WT, int F>
+struct I8ResRing {
     int4v wf[4][F];
     uint2 wr[F];
     float4v wdr[F], wmr[F];
-    auto wload = [&](int4v(&slot)[F], int b) {
+    __device__ __forceinline__ void wload(const GemmArgs &g, int slot, int ft0, int b) {
+        const int nkb = g.K >> 5;
         if (b < nkb) {
 #pragma unroll
-            for (int f = 0; f < F; f++) slot[f] = i8_wq(g.Wi, nkb, ft0 + f, b);
+            for (int f = 0; f < F; f++) wf[slot][f] = i8_wq(g.Wi, nkb, ft0 + f, b);
         }
-    };
-    auto sload = [&](int c) {  // weight scales of chunk c (4 blocks)
+    }
+    __device__ __forceinline__ void sload(const GemmArgs &g, int ft0, int c) {  // weight scales of chunk c (4 blocks)
+        const int nkb = g.K >> 5, nch = g.K / I8_KC, lane = threadIdx.x & 63;
         if (c < nch) {
 #pragma unroll
             for (int f = 0; f < F; f++) {
-                if constexpr (Q1) {
+                if constexpr (WT == W_Q4_1) {
                     wdr[f] = i8_wvec(g.Wi.d, nkb, ft0 + f, c);
                     wmr[f] = i8_wvec(g.Wi.m, nkb, ft0 + f, c);
                 } else {
@@ -393,39 +389,59 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
                 }
             }
         }
-    };
+    }
+    __device__ __forceinline__ void start(const GemmArgs &g, int ft0) {
+        wload(g, 0, ft0, 0);
+        wload(g, 1, ft0, 1);
+        sload(g, ft0, 0);
+    }
+};
+
+template <int WT, int BM, int F, int T>
+__device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
+                                                     float16v (&acc)[F][T], I8ResRing<WT, F> &ring, int ftn) {
+    constexpr bool Q1 = WT == W_Q4_1;
+    using C = I8Chunk<BM, Q1>;
+    const int lane = threadIdx.x & 63, hh = lane >> 5;
+    const int nch = g.K / I8_KC;
+    const float4v z4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < F; f++)
+#pragma unroll
+        for (int t = 0; t < T; t++) acc[f][t] = float16v{};
     int4v ws[F];
     float4v wd[F], wm[F];
     auto wscale_use = [&]() {
 #pragma unroll
         for (int f = 0; f < F; f++) {
             if constexpr (Q1) {
-                wd[f] = hh ? z4 : wdr[f];
-                wm[f] = wmr[f];
+                wd[f] = hh ? z4 : ring.wdr[f];
+                wm[f] = ring.wmr[f];
             } else {
-                ws[f] = int4v{(int)wr[f].x, (int)wr[f].y, (int)wr[f].x, (int)wr[f].y};
+                ws[f] = int4v{(int)ring.wr[f].x, (int)ring.wr[f].y, (int)ring.wr[f].x, (int)ring.wr[f].y};
             }
         }
     };
-    wload(wf[0], 0);
-    wload(wf[1], 1);
-    sload(0);
 #pragma unroll 1
     for (int c = 0; c < nch; c++) {
         const int b0 = 4 * c;
+        const bool last = c + 1 == nch;
         const char *buf = apanel + c * C::BYTES;
         wscale_use();
-        sload(c + 1);
+        if (!last) ring.sload(g, ft0, c + 1);
+        else if (ftn >= 0) ring.sload(g, ftn, 0);
         I8AOps<T> a0, a1;
         i8_aops<WT, BM, T, 0>(a0, buf, tt0);
-        i8_block<WT, BM, F, T, 0, true>(buf, tt0, wf[0], ws, wd, wm, a0, a1, acc);
-        wload(wf[2], b0 + 2);
-        i8_block<WT, BM, F, T, 1, true>(buf, tt0, wf[1], ws, wd, wm, a1, a0, acc);
-        wload(wf[3], b0 + 3);
-        i8_block<WT, BM, F, T, 2, true>(buf, tt0, wf[2], ws, wd, wm, a0, a1, acc);
-        wload(wf[0], b0 + 4);
-        i8_block<WT, BM, F, T, 3, true>(buf, tt0, wf[3], ws, wd, wm, a1, a0, acc);
-        wload(wf[1], b0 + 5);
+        i8_block<WT, BM, F, T, 0, true>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
+        ring.wload(g, 2, ft0, b0 + 2);
+        i8_block<WT, BM, F, T, 1, true>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
+        ring.wload(g, 3, ft0, b0 + 3);
+        i8_block<WT, BM, F, T, 2, true>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
+        if (!last) ring.wload(g, 0, ft0, b0 + 4);
+        else if (ftn >= 0) ring.wload(g, 0, ftn, 0);
+        i8_block<WT, BM, F, T, 3, true>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
+        if (!last) ring.wload(g, 1, ft0, b0 + 5);
+        else if (ftn >= 0) ring.wload(g, 1, ftn, 1);
     }
 }
 

@@ -1633,20 +1633,26 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         // 64 (w & 1) .. + 63 as two 32-token t-tiles; lane (r, hh) holds token
         // 32 t + r of its t-tile t, head dims 16 hh .. 16 hh + 15 (i8_core.h)
         const int part = wv >> 1, tt0 = 2 * (wv & 1);
+        I8ResRing<WT, 1> ring;  // head p + 1's first weight blocks load during head p's split and barriers
+        ring.start(g, part);
         for (int p = 0; p <= H; p++) {
             float16v acc[1][2];
-            if (p < H) i8_resident_mainloop<WT, BM, 1, 2>(g, apanel, 3 * p + part, tt0, acc);
-            STAMP(p, 1, NW);
-            __syncthreads();  // X: the consumers are done with head p - 1's tiles
+            // head p's bias is loaded before its main loop: loaded after it, its wait
+            // would also wait for head p + 1's weight blocks the main loop's end issues
+            const int f0 = p * 3 * D + part * D + 16 * hh;  // head-major feature of acc[..][0]
+            float bias[16];
             if (p < H) {
-                const int f0 = p * 3 * D + part * D + 16 * hh;  // head-major feature of acc[..][0]
-                float bias[16];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
 #pragma unroll
                     for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
                 }
+                i8_resident_mainloop<WT, BM, 1, 2>(g, apanel, 3 * p + part, tt0, acc, ring, p + 1 < H ? 3 * (p + 1) + part : -1);
+            }
+            STAMP(p, 1, NW);
+            __syncthreads();  // X: the consumers are done with head p - 1's tiles
+            if (p < H) {
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
                     const int row = 32 * (tt0 + t) + r;  // tile row (token of the tile)

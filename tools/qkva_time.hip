@@ -64,11 +64,30 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(d_comp, comp.data(), comp.size() * 2, hipMemcpyHostToDevice));
 
     GemmArgs g{};
-    void *aq;
-    CK(hipMalloc(&aq, (size_t)Mpad * E));
-    CK(hipMemset(aq, 0x11, (size_t)Mpad * E));
-    g.A.q = aq;
-    g.A.d = dev_random((size_t)Mpad * (E / 32) * 4, 2, 1);
+    // Q8 activations: random codes in [-127, 127], fp16 block scales near 0.02
+    // (a realistic score spread for the softmax; constant inputs make every
+    // exp-table read one address)
+    {
+        std::vector<int8_t> q((size_t)Mpad * E);
+        uint32_t x = 12345;
+        for (auto &v : q) {
+            x = x * 1664525u + 1013904223u;
+            v = (int8_t)((int)((x >> 24) % 255) - 127);
+        }
+        void *aq;
+        CK(hipMalloc(&aq, q.size()));
+        CK(hipMemcpy(aq, q.data(), q.size(), hipMemcpyHostToDevice));
+        g.A.q = aq;
+        std::vector<uint16_t> d((size_t)Mpad * (E / 32));
+        for (auto &v : d) {
+            x = x * 1664525u + 1013904223u;
+            v = h16(0.01f + 0.02f * (float)(x >> 8) * 0x1p-24f);
+        }
+        void *ad;
+        CK(hipMalloc(&ad, d.size() * 2));
+        CK(hipMemcpy(ad, d.data(), d.size() * 2, hipMemcpyHostToDevice));
+        g.A.d = ad;
+    }
     g.W.q = dev_random((size_t)3 * E * E * 4, 3, 1);
     g.W.unscale = 1.0f / 16384;
     g.bias = (const float *)dev_random((size_t)3 * E * 4, 4, 0);
@@ -88,7 +107,11 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&dq, wq.size()));
         CK(hipMemcpy(dq, wq.data(), wq.size(), hipMemcpyHostToDevice));
         g.Wi.q = (const int8_t *)dq;
-        std::vector<uint16_t> dh((size_t)3 * E * (E / 32), h16(0.01f));
+        std::vector<uint16_t> dh((size_t)3 * E * (E / 32));
+        for (auto &v : dh) {
+            x = x * 1664525u + 1013904223u;
+            v = h16(0.005f + 0.01f * (float)(x >> 8) * 0x1p-24f);
+        }
         void *dd;
         CK(hipMalloc(&dd, dh.size() * 2));
         CK(hipMemcpy(dd, dh.data(), dh.size() * 2, hipMemcpyHostToDevice));
