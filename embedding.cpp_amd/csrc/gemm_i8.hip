@@ -37,6 +37,9 @@ namespace bertamd {
 #ifndef I8_UP_T
 #define I8_UP_T 2
 #endif
+#ifndef I8_UP_AHEAD
+#define I8_UP_AHEAD 3  // weight blocks in flight (i8_core.h I8Pipe)
+#endif
 
 
 // ---------------------------------------------------------------------------
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
     int64_t m0;
     int ft0;
     coords(blockIdx.x, m0, ft0);
-    I8Pipe<WT, NT, BM, F> pp;
+    I8Pipe<WT, NT, BM, F, I8_UP_AHEAD> pp;
     pp.prime(g, m0, ft0);
     for (int tile = blockIdx.x, it = 0; tile < nwg; tile += gridDim.x, it++) {
         int64_t m0n = m0;

@@ -134,8 +134,13 @@ __device__ __forceinline__ void i8_aops(I8AOps<T> &o, const char *buf, int tt0) 
 // an exact vmcnt (an older slow A load never blocks a younger weight wait).
 // The last blocks of a tile load the first blocks / chunk of the workgroup's
 // next tile.
-template <int WT, int NT, int BM, int F>
+// AH: weight blocks in flight ahead of the block being computed (2: a slot is
+// refilled two blocks after it is consumed; 3: one block after — the lead of a
+// 6-slot ring with the registers of 4, where the kernel's register budget has
+// room for the longer live ranges).
+template <int WT, int NT, int BM, int F, int AH = 2>
 struct I8Pipe {
+    static_assert(AH == 2 || AH == 3, "2 or 3 weight blocks ahead");
     static constexpr int IT = (4 * BM + NT - 1) / NT;
     I8Items<IT> st;
     int4v wf[4][F];
@@ -170,6 +175,7 @@ struct I8Pipe {
         const int nkb = g.K >> 5;
         wload<0>(g, nkb, ft0, ft0, 0);
         wload<1>(g, nkb, ft0, ft0, 1);
+        if constexpr (AH == 3) wload<2>(g, nkb, ft0, ft0, 2);
         cload(g, m0, ft0, 0);
     }
 };
@@ -258,9 +264,9 @@ struct I8NoHook {
 // ft0n) on return.  Returns after a final barrier (the LDS may be reused).
 // hook(c, nch) runs at the start of every chunk c, after that chunk's barrier
 // (memory traffic of the caller's epilogue interleaved with the main loop).
-template <int WT, int NT, int BM, int F, int T, bool PIPE = true, typename Hook = I8NoHook>
+template <int WT, int NT, int BM, int F, int T, bool PIPE = true, typename Hook = I8NoHook, int AH = 2>
 __device__ __forceinline__ void i8_mainloop(const GemmArgs &g, int64_t m0, int ft0, int tt0, int64_t m0n, int ft0n,
-                                            char *smem, I8Pipe<WT, NT, BM, F> &pp, float16v (&acc)[F][T],
+                                            char *smem, I8Pipe<WT, NT, BM, F, AH> &pp, float16v (&acc)[F][T],
                                             const Hook &hook = Hook()) {
     constexpr bool Q1 = WT == W_Q4_1;
     using C = I8Chunk<BM, Q1>;
@@ -296,15 +302,16 @@ __device__ __forceinline__ void i8_mainloop(const GemmArgs &g, int64_t m0, int f
         hook(c, nch);
         I8AOps<T> a0, a1;
         i8_aops<WT, BM, T, 0>(a0, buf, tt0);
+        constexpr int A = AH;
         i8_block<WT, BM, F, T, 0, PIPE>(buf, tt0, pp.wf[0], ws, wd, wm, a0, a1, acc);
-        pp.template wload<2>(g, nkb, ft0, ft0n, b0 + 2);
+        pp.template wload<(0 + A) & 3>(g, nkb, ft0, ft0n, b0 + 0 + A);
         i8_block<WT, BM, F, T, 1, PIPE>(buf, tt0, pp.wf[1], ws, wd, wm, a1, a0, acc);
-        pp.template wload<3>(g, nkb, ft0, ft0n, b0 + 3);
+        pp.template wload<(1 + A) & 3>(g, nkb, ft0, ft0n, b0 + 1 + A);
         pp.cload(g, more ? m0 : m0n, more ? ft0 : ft0n, more ? c + 1 : 0);
         i8_block<WT, BM, F, T, 2, PIPE>(buf, tt0, pp.wf[2], ws, wd, wm, a0, a1, acc);
-        pp.template wload<0>(g, nkb, ft0, ft0n, b0 + 4);
+        pp.template wload<(2 + A) & 3>(g, nkb, ft0, ft0n, b0 + 2 + A);
         i8_block<WT, BM, F, T, 3, PIPE>(buf, tt0, pp.wf[3], ws, wd, wm, a1, a0, acc);
-        pp.template wload<1>(g, nkb, ft0, ft0n, b0 + 5);
+        pp.template wload<(3 + A) & 3>(g, nkb, ft0, ft0n, b0 + 3 + A);
         if (more) {
             i8_stage_store<WT, BM, NT>(pp.st, smem + ((c + 1) & 1) * C::BYTES);
             wscale_use();
@@ -364,7 +371,7 @@ namespace bertamd {
 // two blocks and scales; each call consumes the ring for ft0 and, when ftn >= 0,
 // refills it with f-tile ftn's first blocks and scales at its end, so their
 // L2 latency passes during whatever the caller does between two calls.
-template <int WT, int F>
+template <int WT, int F, int AH = 2>
 struct I8ResRing {
     int4v wf[4][F];
     uint2 wr[F];
@@ -393,13 +400,14 @@ struct I8ResRing {
     __device__ __forceinline__ void start(const GemmArgs &g, int ft0) {
         wload(g, 0, ft0, 0);
         wload(g, 1, ft0, 1);
+        if constexpr (AH == 3) wload(g, 2, ft0, 2);
         sload(g, ft0, 0);
     }
 };
 
-template <int WT, int BM, int F, int T>
+template <int WT, int BM, int F, int T, int AH>
 __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
-                                                     float16v (&acc)[F][T], I8ResRing<WT, F> &ring, int ftn) {
+                                                     float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn) {
     constexpr bool Q1 = WT == W_Q4_1;
     using C = I8Chunk<BM, Q1>;
     const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -432,16 +440,22 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
         else if (ftn >= 0) ring.sload(g, ftn, 0);
         I8AOps<T> a0, a1;
         i8_aops<WT, BM, T, 0>(a0, buf, tt0);
+        // block b0 + j + A into slot (j + A) & 3; past the f-tile's last block,
+        // the first blocks of f-tile ftn
+        constexpr int A = AH;
+        auto refill = [&](int j) {
+            const int b = b0 + j + A;
+            if (b < 4 * nch) ring.wload(g, (j + A) & 3, ft0, b);
+            else if (ftn >= 0) ring.wload(g, (j + A) & 3, ftn, b - 4 * nch);
+        };
         i8_block<WT, BM, F, T, 0, true>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
-        ring.wload(g, 2, ft0, b0 + 2);
+        refill(0);
         i8_block<WT, BM, F, T, 1, true>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
-        ring.wload(g, 3, ft0, b0 + 3);
+        refill(1);
         i8_block<WT, BM, F, T, 2, true>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
-        if (!last) ring.wload(g, 0, ft0, b0 + 4);
-        else if (ftn >= 0) ring.wload(g, 0, ftn, 0);
+        refill(2);
         i8_block<WT, BM, F, T, 3, true>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
-        if (!last) ring.wload(g, 1, ft0, b0 + 5);
-        else if (ftn >= 0) ring.wload(g, 1, ftn, 1);
+        refill(3);
     }
 }
 

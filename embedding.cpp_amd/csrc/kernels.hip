@@ -1561,6 +1561,9 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 // tiles; the tiles hold the next head).  LDS: the panel (58 KB), one head's
 // tiles (57 KB), the exp table (40 KB).
 constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
+#ifndef QKPC_AHEAD
+#define QKPC_AHEAD 2  // the producers' weight blocks in flight (i8_core.h I8ResRing)
+#endif
 #ifndef QKPC_CPRIO
 #define QKPC_CPRIO 0  // static issue priority of the consumer waves (A/B)
 #endif
@@ -1633,7 +1636,7 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         // 64 (w & 1) .. + 63 as two 32-token t-tiles; lane (r, hh) holds token
         // 32 t + r of its t-tile t, head dims 16 hh .. 16 hh + 15 (i8_core.h)
         const int part = wv >> 1, tt0 = 2 * (wv & 1);
-        I8ResRing<WT, 1> ring;  // head p + 1's first weight blocks load during head p's split and barriers
+        I8ResRing<WT, 1, QKPC_AHEAD> ring;  // head p + 1's first weight blocks load during head p's split and barriers
         ring.start(g, part);
         for (int p = 0; p <= H; p++) {
             float16v acc[1][2];
