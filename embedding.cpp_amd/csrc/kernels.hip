@@ -1728,11 +1728,11 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
             sum = 0;
             if (act) {
                 const int nkt = (len + 31) >> 5;
-                int klim = lim;  // key 32 kt + (j & 3) + 8 (j >> 2) + 4 hh valid while < len
-                if constexpr (PK) {
-                    klim = len - 4 * hh;
-                    asm volatile("" : "+v"(klim));
-                }
+                // key 32 kt + (j & 3) + 8 (j >> 2) + 4 hh valid while < len.  Opaque per
+                // head: loop-invariant, the 64 mask compares were hoisted out of the head
+                // loop as 64-bit lane masks and spilled the SGPRs
+                int klim = PK ? len - 4 * hh : lim;
+                asm volatile("" : "+v"(klim));
                 half8 qh[D / 16], ql[D / 16];
 #pragma unroll
                 for (int ks = 0; ks < D / 16; ks++) {
