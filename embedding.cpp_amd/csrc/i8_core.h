@@ -182,11 +182,7 @@ struct I8Pipe {
 
 // One quant block (BB = its index inside the chunk) of the main loop, with
 // its activation operands `cur` (the next block's are read into `nxt`).
-// SW (Q4_0): the MFMA operands swapped, so the 32 x 32 results are transposed —
-// lane (r, hh) holds weight row r of the f-tile (feature 16 ((r >> 2) & 1) +
-// 4 (r >> 3) + (r & 3)) for the tokens 8 (i / 4) + 4 hh + i % 4 of its t-tile in
-// register i; the same products and sums, so the same bits.
-template <int WT, int BM, int F, int T, int BB, bool PIPE, bool SW = false>
+template <int WT, int BM, int F, int T, int BB, bool PIPE>
 __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (&wfc)[F], const int4v (&ws)[F],
                                          const float4v (&wd)[F], const float4v (&wm)[F], const I8AOps<T> &cur,
                                          I8AOps<T> &nxt, float16v (&acc)[F][T]) {
@@ -217,36 +213,30 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
             oh[t][BB >> 1] = (int)v;
         }
     }
-    static_assert(!SW || WT == W_Q4_0, "swapped operands: Q4_0 only");
     auto ddmfma = [&](int f, int t) {
-        if constexpr (SW)
-            return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, oh[t]),
-                                                          __builtin_bit_cast(half8, ws[f]), zf, 0, 0, 0);
-        else if constexpr (WT == W_Q4_0)
+        if constexpr (WT == W_Q4_0)
             return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ws[f]),
                                                           __builtin_bit_cast(half8, oh[t]), zf, 0, 0, 0);
         else
             return __builtin_amdgcn_mfma_f32_32x32x2f32(wd[f][BB], cur.da[t], zf, 0, 0, 0);
-    };
-    auto ismfma = [&](int f, int t) {
-        return SW ? __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xa[t], wfc[f], __builtin_bit_cast(int16v, zf), 0, 0, 0)
-                  : __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[f], cur.xa[t], __builtin_bit_cast(int16v, zf), 0, 0, 0);
     };
     // software pipeline over the F x T tiles: tile p + 1's two MFMAs are in
     // flight while tile p is folded
     // (PIPE false: issue and fold tile by tile; latency left to other waves)
     int16v is[2];
     float16v dd[2];
-    is[0] = ismfma(0, 0);
+    is[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[0], cur.xa[0], __builtin_bit_cast(int16v, zf), 0, 0, 0);
     dd[0] = ddmfma(0, 0);
 #pragma unroll
     for (int p = 0; p < F * T; p++) {
         if (!PIPE && p > 0) {
-            is[p & 1] = ismfma(p / T, p % T);
+            is[p & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[p / T], cur.xa[p % T], __builtin_bit_cast(int16v, zf),
+                                                              0, 0, 0);
             dd[p & 1] = ddmfma(p / T, p % T);
         }
         if (PIPE && p + 1 < F * T) {
-            is[(p + 1) & 1] = ismfma((p + 1) / T, (p + 1) % T);
+            is[(p + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[(p + 1) / T], cur.xa[(p + 1) % T],
+                                                                     __builtin_bit_cast(int16v, zf), 0, 0, 0);
             dd[(p + 1) & 1] = ddmfma((p + 1) / T, (p + 1) % T);
         }
         // tile p + 1's MFMAs are issued before tile p's fold reads tile p's
@@ -415,7 +405,7 @@ struct I8ResRing {
     }
 };
 
-template <int WT, int BM, int F, int T, int AH, bool SW = false>
+template <int WT, int BM, int F, int T, int AH>
 __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
                                                      float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn) {
     constexpr bool Q1 = WT == W_Q4_1;
@@ -458,13 +448,13 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
             if (b < 4 * nch) ring.wload(g, (j + A) & 3, ft0, b);
             else if (ftn >= 0) ring.wload(g, (j + A) & 3, ftn, b - 4 * nch);
         };
-        i8_block<WT, BM, F, T, 0, true, SW>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
+        i8_block<WT, BM, F, T, 0, true>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
         refill(0);
-        i8_block<WT, BM, F, T, 1, true, SW>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
+        i8_block<WT, BM, F, T, 1, true>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
         refill(1);
-        i8_block<WT, BM, F, T, 2, true, SW>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
+        i8_block<WT, BM, F, T, 2, true>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
         refill(2);
-        i8_block<WT, BM, F, T, 3, true, SW>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
+        i8_block<WT, BM, F, T, 3, true>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
         refill(3);
     }
 }

@@ -1634,100 +1634,62 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
     if (wv < NP) {
         // ---- producer: f-tile 3 h + part (part = w / 2: Q, K, V of head h), tokens
         // 64 (w & 1) .. + 63 as two 32-token t-tiles; lane (r, hh) holds token
-        // 32 t + r of its t-tile t, head dims 16 hh .. 16 hh + 15 (i8_core.h).
-        // V of an unpacked tile (VSW): transposed MFMA results (i8_block SW), lane
-        // (r, hh) = head dim fe, register 4 q + j = key 32 t + 8 q + 4 hh + j, so
-        // V^T leaves in 8-byte runs of 4 key slots instead of 2-byte scatters.  The
-        // two forms are separate loops (one loop with both spills 96 B/lane).
+        // 32 t + r of its t-tile t, head dims 16 hh .. 16 hh + 15 (i8_core.h)
         const int part = wv >> 1, tt0 = 2 * (wv & 1);
-        auto produce = [&](auto vsw_c) {
-            constexpr bool VSW = decltype(vsw_c)::value;
-            I8ResRing<WT, 1, QKPC_AHEAD> ring;  // head p + 1's first weight blocks load during head p's split and barriers
-            ring.start(g, part);
-            const int fe = 16 * ((r >> 2) & 1) + 4 * (r >> 3) + (r & 3);  // (VSW) this lane's head dim
-            for (int p = 0; p <= H; p++) {
-                float16v acc[1][2];
-                // head p's bias is loaded before its main loop: loaded after it, its
-                // wait would also wait for head p + 1's weight blocks the main loop's
-                // end issues
-                float bias[VSW ? 1 : 16];
-                if (p < H) {
-                    if constexpr (VSW) {
-                        bias[0] = g.bias[p * 3 * D + 2 * D + fe];
-                    } else {
-                        const int f0 = p * 3 * D + part * D + 16 * hh;  // head-major feature of acc[..][0]
+        I8ResRing<WT, 1, QKPC_AHEAD> ring;  // head p + 1's first weight blocks load during head p's split and barriers
+        ring.start(g, part);
+        for (int p = 0; p <= H; p++) {
+            float16v acc[1][2];
+            // head p's bias is loaded before its main loop: loaded after it, its wait
+            // would also wait for head p + 1's weight blocks the main loop's end issues
+            const int f0 = p * 3 * D + part * D + 16 * hh;  // head-major feature of acc[..][0]
+            float bias[16];
+            if (p < H) {
 #pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
+                for (int q = 0; q < 4; q++) {
+                    const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
 #pragma unroll
-                            for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
-                        }
-                    }
-                    i8_resident_mainloop<WT, BM, 1, 2, QKPC_AHEAD, VSW>(g, apanel, 3 * p + part, tt0, acc, ring,
-                                                                        p + 1 < H ? 3 * (p + 1) + part : -1);
+                    for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
                 }
-                STAMP(p, 1, NW);
-                __syncthreads();  // X: the consumers are done with head p - 1's tiles
-                if (p < H) {
-#pragma unroll
-                    for (int t = 0; t < 2; t++) {
-                        if constexpr (VSW) {
-                            // keys >= n get finite values of the zero / neighbouring
-                            // panel rows, weighted by p = 0
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                half4v hv, lv;
-#pragma unroll
-                                for (int j = 0; j < 4; j++) {
-                                    const float y = bias[0] + acc[0][t][4 * q + j];
-                                    const _Float16 yh = (_Float16)y;
-                                    hv[j] = yh;
-                                    lv[j] = (_Float16)(y - (float)yh);
-                                }
-                                const int key = 32 * (tt0 + t) + 8 * q + 4 * hh;
-                                *(half4v *)(plane(4) + fe * VST + key) = hv;
-                                *(half4v *)(plane(5) + fe * VST + key) = lv;
-                            }
-                        } else {
-                            const int row = 32 * (tt0 + t) + r;  // tile row (token of the tile)
-                            if (row < n) {                       // rows >= n stay zero
-                                half8 hv[2], lv[2];
-#pragma unroll
-                                for (int i = 0; i < 16; i++) {
-                                    const float y = bias[i] + acc[0][t][i];
-                                    const _Float16 yh = (_Float16)y;
-                                    hv[i >> 3][i & 7] = yh;
-                                    lv[i >> 3][i & 7] = (_Float16)(y - (float)yh);
-                                }
-                                if (part < 2) {  // Q | K: row-major [token][dim]
-                                    _Float16 *ph = plane(2 * part) + row * KST + 16 * hh,
-                                             *pl = plane(2 * part + 1) + row * KST + 16 * hh;
-                                    *(half8 *)ph = hv[0];
-                                    *(half8 *)(ph + 8) = hv[1];
-                                    *(half8 *)pl = lv[0];
-                                    *(half8 *)(pl + 8) = lv[1];
-                                } else {  // V^T [dim][key slot]
-                                    const int slot = PK ? (int)vslot[row] : row;
-                                    _Float16 *ph = plane(4) + (16 * hh) * VST + slot, *pl = plane(5) + (16 * hh) * VST + slot;
-#pragma unroll
-                                    for (int i = 0; i < 16; i++) {
-                                        ph[i * VST] = hv[i >> 3][i & 7];
-                                        pl[i * VST] = lv[i >> 3][i & 7];
-                                    }
-                                }
-                            }
-                        }
-                    }
-                }
-                STAMP(p, 2, NW);
-                __syncthreads();  // Y: head p's tiles are complete
-                STAMP(p + 1, 0, NW);
+                i8_resident_mainloop<WT, BM, 1, 2>(g, apanel, 3 * p + part, tt0, acc, ring, p + 1 < H ? 3 * (p + 1) + part : -1);
             }
-        };
-        if (!PK && part == 2)
-            produce(std::true_type{});
-        else
-            produce(std::false_type{});
+            STAMP(p, 1, NW);
+            __syncthreads();  // X: the consumers are done with head p - 1's tiles
+            if (p < H) {
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int row = 32 * (tt0 + t) + r;  // tile row (token of the tile)
+                    if (row < n) {                       // rows >= n stay zero
+                        half8 hv[2], lv[2];
+#pragma unroll
+                        for (int i = 0; i < 16; i++) {
+                            const float y = bias[i] + acc[0][t][i];
+                            const _Float16 yh = (_Float16)y;
+                            hv[i >> 3][i & 7] = yh;
+                            lv[i >> 3][i & 7] = (_Float16)(y - (float)yh);
+                        }
+                        if (part < 2) {  // Q | K: row-major [token][dim]
+                            _Float16 *ph = plane(2 * part) + row * KST + 16 * hh, *pl = plane(2 * part + 1) + row * KST + 16 * hh;
+                            *(half8 *)ph = hv[0];
+                            *(half8 *)(ph + 8) = hv[1];
+                            *(half8 *)pl = lv[0];
+                            *(half8 *)(pl + 8) = lv[1];
+                        } else {  // V^T [dim][key slot]
+                            const int slot = PK ? (int)vslot[row] : row;
+                            _Float16 *ph = plane(4) + (16 * hh) * VST + slot, *pl = plane(5) + (16 * hh) * VST + slot;
+#pragma unroll
+                            for (int i = 0; i < 16; i++) {
+                                ph[i * VST] = hv[i >> 3][i & 7];
+                                pl[i * VST] = lv[i >> 3][i & 7];
+                            }
+                        }
+                    }
+                }
+            }
+            STAMP(p, 2, NW);
+            __syncthreads();  // Y: head p's tiles are complete
+            STAMP(p + 1, 0, NW);
+        }
     } else {
         // ---- consumer: query block qb of head p - 1 (32 queries of one sentence)
 #if QKPC_CPRIO > 0
