@@ -1564,12 +1564,6 @@ constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
 #ifndef QKPC_AHEAD
 #define QKPC_AHEAD 2  // the producers' weight blocks in flight (i8_core.h I8ResRing)
 #endif
-#ifndef QKPC_CPRIO
-#define QKPC_CPRIO 0  // static issue priority of the consumer waves (A/B)
-#endif
-#ifndef QKPC_DEFER
-#define QKPC_DEFER 0  // consumers store head h's context during head h + 1's period (A/B)
-#endif
 
 template <bool PK>
 __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
@@ -1692,9 +1686,6 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         }
     } else {
         // ---- consumer: query block qb of head p - 1 (32 queries of one sentence)
-#if QKPC_CPRIO > 0
-        __builtin_amdgcn_s_setprio(QKPC_CPRIO);
-#endif
         const int qb = wv - NP;
         int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
         asm volatile("" : "+v"(lim));
@@ -1721,10 +1712,6 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         for (int p = 0; p <= H; p++) {
             const int head = p - 1;
             const bool act = head >= 0 && qact;
-#if QKPC_DEFER
-            // head p - 2's context leaves now, beside the producers' main loop
-            if (act && head >= 1) store_ctx(head - 1);
-#endif
             sum = 0;
             if (act) {
                 const int nkt = (len + 31) >> 5;
@@ -1790,16 +1777,11 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
             }
             STAMP(p, 1, NW);
             __syncthreads();  // X: this head's tiles may be overwritten
-#if !QKPC_DEFER
             if (act) store_ctx(head);
-#endif
             STAMP(p, 2, NW);
             __syncthreads();  // Y
             STAMP(p + 1, 0, NW);
         }
-#if QKPC_DEFER
-        if (qact && H >= 1) store_ctx(H - 1);
-#endif
     }
 }
 
