@@ -130,6 +130,9 @@ __device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ 
 #ifndef I8_LN_OV
 #define I8_LN_OV 1
 #endif
+#ifndef I8_LN_AHEAD
+X
+#endif
 
 template <int WT, bool OV = I8_LN_OV>
 __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles) {
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
     const int col = 32 * ft0 + 16 * hh;
     if ((int)blockIdx.x >= n_mtiles) return;
     int64_t m0n = (int64_t)xcd_linear(blockIdx.x, n_mtiles) * BM;
-    I8Pipe<WT, NT, BM, F> pp;
+    I8Pipe<WT, NT, BM, F, I8_LN_AHEAD> pp;
     pp.prime(g, m0n, ft0);
     // wave w's piece k: LDS chunks 64 (8 w + k) .. + 63 of xs, i.e. lane l holds
     // chunk j = 64 (8 w + k) + l = (row r, column chunk cs ^ (r & 15)) of the tile
