@@ -35,7 +35,6 @@ METRIC = "embeddings/sec at seq_len=128 batch=1024; cosine-sim vs ggml CPU ref"
 PEAK_FP16_TFLOPS = 2516.6  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP32_MFMA_TFLOPS = 157.3
 PEAK_INT8_TOPS = 2 * PEAK_FP16_TFLOPS  # i8 MFMA: 2x the bf16 rate per clock (MI355X_MICROARCH.md MFMA table)
-I8_KERNELS = ("gemm_up_gelu", "gemm_down_ln")  # the int8-MFMA GEMMs of the Q4 models
 PEAK_HBM_GBS = 8000.0
 
 
@@ -137,16 +136,75 @@ def build_info() -> dict:
 
 
 def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
+    return sum(f for f, _ in kernel_parts(name, B, N, hp, {}, "q4_0"))
+
+
+def kernel_parts(name: str, B: int, N: int, hp: dict, arith: dict, ftype: str) -> list:
+    """Algorithmic work of one launch split by the MFMA arithmetic it runs on:
+    [(flops, peak TFLOP/s)].  `arith` is the library's resolved choice per
+    projection (bert_amd_get_option: qkva_ntw, i8_up / i8_o / i8_down): a Q4
+    projection on the int8-MFMA GEMMs is priced at the int8 peak, one on the
+    split-fp16 GEMMs at the fp16 peak; attention (split-fp16 K.Q and P.V) at
+    the fp16 peak; F32 GEMMs at the fp32 MFMA peak."""
     E, I = hp["n_embd"], hp["n_intermediate"]
     M = B * N
+    q4 = ftype in ("q4_0", "q4_1")
+    gemm_peak = PEAK_FP32_MFMA_TFLOPS if ftype == "f32" else PEAK_FP16_TFLOPS
+
+    def proj(key):
+        return PEAK_INT8_TOPS if q4 and arith.get(key) else gemm_peak
+
+    qkv_int8 = q4 and arith.get("qkva_ntw") == 0  # producer / consumer kernel and its unfused twin
+    qkv = (2.0 * M * E * 3 * E, PEAK_INT8_TOPS if qkv_int8 else gemm_peak)
+    att = (4.0 * B * N * N * E, PEAK_FP16_TFLOPS)
     return {
-        "gemm_qkv": 2.0 * M * E * 3 * E,
-        "gemm_o_ln": 2.0 * M * E * E,
-        "gemm_up_gelu": 2.0 * M * E * I,
-        "gemm_down_ln": 2.0 * M * I * E,
-        "attention": 4.0 * B * N * N * E,
-        "qkv_attention": 2.0 * M * E * 3 * E + 4.0 * B * N * N * E,
-    }.get(name, 0.0)
+        "gemm_qkv": [qkv],
+        "gemm_o_ln": [(2.0 * M * E * E, proj("i8_o"))],
+        "gemm_up_gelu": [(2.0 * M * E * I, proj("i8_up"))],
+        "gemm_down_ln": [(2.0 * M * I * E, proj("i8_down"))],
+        "attention": [att],
+        "qkv_attention": [qkv, att],
+    }.get(name, [])
+
+
+def dtype_label(ftype: str, arith: dict) -> str:
+    """The MFMA arithmetic of the step: Q4 models run their int8-MFMA
+    projections (exact Q4 x Q8 block dots) beside split-fp16 ones and fp16
+    attention."""
+    if ftype in ("q4_0", "q4_1"):
+        i8 = arith.get("qkva_ntw") == 0 or any(arith.get(k) for k in ("i8_up", "i8_o", "i8_down"))
+        return "int8+fp16" if i8 else "fp16"
+    return "fp32+fp16" if ftype == "f32" else "fp16"
+
+
+def dtype_note(ftype: str, arith: dict) -> str:
+    if ftype in ("q4_0", "q4_1"):
+        names = {"qkv": arith.get("qkva_ntw") == 0, "o": arith.get("i8_o"), "up": arith.get("i8_up"),
+                 "down": arith.get("i8_down")}
+        i8 = [k for k, v in names.items() if v]
+        f16 = [k for k, v in names.items() if not v]
+        s = "Q4 x Q8 as ggml vec_dot_q4_x_q8_x: "
+        if i8:
+            s += f"{'/'.join(i8)} on int8 MFMA (exact block isum, per-block d_w*d_a fold in f32)"
+        if f16:
+            s += ("; " if i8 else "") + (f"{'/'.join(f16)} with Q4 weights as exact fp16 hi/lo pairs x Q8 integers "
+                                         "on fp16 MFMA (per-block d_a fold)")
+    else:
+        s = f"{ftype} GEMM on {'fp16' if ftype == 'f16' else 'f32'} MFMA, f32 accumulate"
+    return s + "; attention split-fp16 MFMA (f32-level); LN/softmax sums f64"
+
+
+def mixed_roofline(parts: list, avg_s: float) -> dict:
+    """frac = (sum of F_i / P_i) / t: the launch's ideal time at each part's
+    own peak over its measured time.  `peak` is the matching effective peak
+    (F / ideal time), so achieved / peak == frac."""
+    fl = sum(f for f, _ in parts)
+    ideal = sum(f / (p * 1e12) for f, p in parts)
+    dts = sorted({"int8" if p == PEAK_INT8_TOPS else "fp32" if p == PEAK_FP32_MFMA_TFLOPS else "fp16"
+                  for _, p in parts}, key=["int8", "fp16", "fp32"].index)
+    return dict(achieved=round(fl / avg_s / 1e12, 1), peak=round(fl / ideal / 1e12, 1), frac=round(ideal / avg_s, 4),
+                flops_per_launch=fl, peak_dtype="+".join(dts),
+                parts=[dict(flops=f, peak=p) for f, p in parts])
 
 
 def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
@@ -280,6 +338,8 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--pmc-csv", default=os.environ.get("BENCH_PMC_CSV", ""))
     ap.add_argument("--host-runs", type=int, default=10, help="timed bert_eval_batch runs (host buffers), 0: skip")
+    ap.add_argument("--load-replicas", type=int, default=8, help="time a load with this many replicas on one device")
+    ap.add_argument("--latency-runs", type=int, default=100, help="single-sentence bert_eval runs per length, 0: skip")
     ap.add_argument("--ragged-steps", type=int, default=10, help="variable-length batch steps, 0: skip")
     ap.add_argument("--consumer-texts", type=int, default=4096,
                     help="texts for the bert_encode_batch (consumer path) line, 0: skip")
@@ -332,7 +392,9 @@ def main():
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
+        l0 = time.perf_counter()
         model = bertlib.BertModel(path, devices=[gpu])
+        load_s = time.perf_counter() - l0
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -380,30 +442,30 @@ def main():
     prof = model.profile_read()
     model.profile(False)
     model.set_option("split", int(os.environ.get("BERT_AMD_SPLIT", "1")[:1] != "0"))
+    arith = {k: model.get_option(k) for k in ("qkva_ntw", "i8_up", "i8_o", "i8_down")}
     kern = {}
     for name, (ms, cnt) in prof.items():
-        fl = kernel_flops(name, B, N, hp)
+        parts = kernel_parts(name, B, N, hp, arith, args.ftype)
         by = kernel_bytes(name, B, N, hp, args.ftype)
         avg_s = ms / max(cnt, 1) / 1e3
         kern[name] = dict(avg_us=round(avg_s * 1e6, 2), launches_per_step=cnt // max(args.profile_steps, 1),
                           share=round(ms / max(sum(v[0] for v in prof.values()), 1e-9), 4),
-                          tflops=round(fl / avg_s / 1e12, 1) if fl else None,
                           gbs=round(by / avg_s / 1e9, 1) if by else None)
+        if parts:
+            mr = mixed_roofline(parts, avg_s)
+            kern[name].update(tflops=mr["achieved"], mfma_frac=mr["frac"], peak_dtype=mr["peak_dtype"])
     dominant = max(prof, key=lambda k: prof[k][0]) if prof else None
 
     roofline = None
     hbm_step = None
     if dominant:
         avg_s = prof[dominant][0] / prof[dominant][1] / 1e3
-        fl = kernel_flops(dominant, B, N, hp)
-        if fl:
-            peak = PEAK_FP32_MFMA_TFLOPS if (args.ftype == "f32" and dominant != "attention") else PEAK_FP16_TFLOPS
-            pdt = "fp32" if args.ftype == "f32" and dominant != "attention" else "fp16"
-            if args.ftype in ("q4_0", "q4_1") and dominant in I8_KERNELS:
-                peak, pdt = PEAK_INT8_TOPS, "int8"  # priced against the int8 MFMA it runs on
-            ach = fl / avg_s / 1e12
-            roofline = dict(kernel=dominant, bound="mfma", achieved=round(ach, 1), peak=peak, unit="TFLOP/s",
-                            frac=round(ach / peak, 4), flops_per_launch=fl, peak_dtype=pdt)
+        parts = kernel_parts(dominant, B, N, hp, arith, args.ftype)
+        if parts:
+            # priced on the arithmetic each part runs (mixed_roofline); e.g. the
+            # producer / consumer kernel: QKV at the int8 peak, attention at fp16
+            roofline = dict(kernel=dominant, bound="mfma", unit="TFLOP/s", **mixed_roofline(parts, avg_s),
+                            formula="frac = sum(F_i / peak_i) / t_launch; peak = F / sum(F_i / peak_i)")
         else:
             by = kernel_bytes(dominant, B, N, hp, args.ftype)
             ach = by / avg_s / 1e9
@@ -448,6 +510,11 @@ def main():
     E, I, L = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
     f_sent = L * (8 * N * E * E + 4 * N * E * I + 4 * N * N * E)
     path_frac = f_sent * value / (world * PEAK_FP16_TFLOPS * 1e12)
+    # the same step priced on the arithmetic each projection runs (int8 / fp16):
+    # the ideal step time at those peaks over the measured ms_per_step
+    ideal_step = L * sum(f / (p * 1e12) for k in ("gemm_qkv", "attention", "gemm_o_ln", "gemm_up_gelu", "gemm_down_ln")
+                         for f, p in kernel_parts(k, B, N, hp, arith, args.ftype))
+    path_frac_mixed = ideal_step / (ms_per_step * 1e-3)
 
     # the reference ABI path (bert_eval_batch: host token lists in, host rows out,
     # pinned H2D of the ids and D2H of the embeddings included), SURVEY §8(d):
@@ -467,6 +534,37 @@ def main():
         host_api = dict(value=round(B / med, 1), unit="embeddings/s", ms_median=round(med * 1e3, 3),
                         ms_min=round(min(ts) * 1e3, 3), runs=args.host_runs,
                         note="bert_eval_batch on host buffers, per GPU: ids H2D + embeddings D2H included")
+
+    # single-sentence latency: the reference server's path (examples/server.cpp:114
+    # -> bert_encode -> bert_eval, one text per request; bert.cpp:1020-1028):
+    # bert_eval on host buffers, median of `latency_runs` after 10 warm-ups, at
+    # N = 16 / 32 / 128 tokens, with the kernel launches one call makes
+    latency = None
+    if args.latency_runs > 0:
+        log("single-sentence latency (bert_eval)")
+        latency = {}
+        for n_tok in (16, 32, 128):
+            sent = toks[0][:n_tok].copy()
+            sent[-1] = 102
+            for _ in range(10):
+                model.eval(sent)
+            ts = []
+            for _ in range(args.latency_runs):
+                h0 = time.perf_counter()
+                model.eval(sent)
+                ts.append(time.perf_counter() - h0)
+            model.profile(True)
+            model.eval(sent)
+            lp = model.profile_read()
+            model.profile(False)
+            latency[f"n{n_tok}"] = dict(us_median=round(float(np.median(ts)) * 1e6, 1),
+                                        us_p10=round(float(np.percentile(ts, 10)) * 1e6, 1),
+                                        us_p90=round(float(np.percentile(ts, 90)) * 1e6, 1),
+                                        launches_per_call=int(sum(c for _, c in lp.values())),
+                                        device_us=round(sum(ms for ms, _ in lp.values()) * 1e3, 1))
+        latency["note"] = ("bert_eval, one sentence, host buffers (ids H2D + embedding D2H + stream sync), "
+                           f"median of {args.latency_runs}; device_us = sum of the call's kernel durations "
+                           "(HIP events, separate profiled call)")
 
     # variable-length batches (server / MTEB-like sentences), same sentence
     # count, device-resident like the headline: lengths uniform in [8, 128],
@@ -561,6 +659,26 @@ def main():
         parity = dict(cos_min=float(c.min()), cos_mean=float(c.mean()), n=S,
                       max_abs=float(np.abs(out[:S] - ref).max()))
 
+    # model load: one replica (above) vs 8 replicas on this one device
+    # (rehearsal of an 8-GPU bert_load_from_file: the weights are repacked
+    # once and uploaded by one thread per replica, runtime.cpp Stager)
+    load = None
+    if rank == 0 and args.load_replicas > 1:
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            l0 = time.perf_counter()
+            mr = bertlib.BertModel(path, devices=[gpu] * args.load_replicas)
+            lr = time.perf_counter() - l0
+            mr.close()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+        load = dict(one_replica_s=round(load_s, 3), replicas=args.load_replicas, replicas_s=round(lr, 3),
+                    note=f"bert_amd_load wall time; {args.load_replicas} replicas all on device {gpu} "
+                         "(one repack, one upload thread per replica)")
+
     # N > 1: the library's own sharding, the path drop-in consumers get
     # (bert_amd_load over every device of the node + bert_eval_batch on host
     # buffers: one thread per device, slices balanced by token count), on the
@@ -580,12 +698,9 @@ def main():
         res = {
             "metric": METRIC, "value": round(value, 1), "unit": "embeddings/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
-            "dtype_note": ("Q4 x Q8 (ggml vec_dot_q4_x_q8_x): FFN-up (and FFN-down at E=384) on int8 MFMA, exact "
-                           "block isum, per-block d_w*d_a fold in f32; QKV / O with Q4 weights as exact fp16 hi/lo "
-                           "pairs x Q8 integers on fp16 MFMA, per-block d_a fold" if args.ftype.startswith("q")
-                           else f"{args.ftype} GEMM on {'fp16' if args.ftype == 'f16' else 'f32'} MFMA, f32 accumulate")
-                          + "; attention split-fp16 MFMA (f32-level); LN/softmax sums f64",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": dtype_label(args.ftype, arith),
+            "dtype_note": dtype_note(args.ftype, arith),
             "data": "synthetic (deterministic splitmix64 token ids and weights; no checkpoints offline)",
             "config": {"workload": f"{args.shape} {args.ftype} batch={B} seq_len={N} per GPU",
                        "model": f"all-MiniLM-L6-v2 shape ({args.shape}), synthetic weights" if args.shape == "minilm"
@@ -594,16 +709,19 @@ def main():
             "roofline": roofline,
             "build": build_info(),
             "pipeline_mfma_frac": round(path_frac, 4),
+            "pipeline_mfma_frac_mixed": round(path_frac_mixed, 4),
             "step_hbm": hbm_step,
             "kernels": kern,
             "kernels_note": "per-kernel HIP-event pass with one row group (bert_amd_set_option split 0); the timed steps "
                             "run two row groups on two streams (runtime.cpp run_pipeline)",
             "cosine_vs_oracle": parity,
             "host_api": host_api,
+            "latency": latency,
             "ragged": ragged,
             "ragged_short": ragged_short,
             "consumer": consumer,
             "library_sharding": lib_shard,
+            "load": load,
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)

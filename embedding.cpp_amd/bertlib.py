@@ -36,7 +36,7 @@ EXT_SYMBOLS = [
     "bert_amd_load", "bert_amd_n_devices", "bert_amd_hparams", "bert_amd_eval_device",
     "bert_amd_profile_enable", "bert_amd_profile_read", "bert_amd_synth_model", "bert_amd_tokenize_json",
     "bert_amd_debug_embed", "bert_amd_workspace_rows", "bert_amd_last_error", "bert_amd_load_opts",
-    "bert_amd_debug_layers", "bert_amd_set_option",
+    "bert_amd_debug_layers", "bert_amd_set_option", "bert_amd_get_option", "bert_amd_shard_cuts",
 ]
 
 # model shapes of BASELINE.json's configs
@@ -102,6 +102,10 @@ def lib() -> ctypes.CDLL:
     L.bert_amd_debug_layers.argtypes = [ctypes.c_void_p, I_P, I_P, ctypes.c_int32, F_P, ctypes.c_void_p, ctypes.c_void_p]
     L.bert_amd_set_option.restype = ctypes.c_int32
     L.bert_amd_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
+    L.bert_amd_get_option.restype = ctypes.c_int32
+    L.bert_amd_get_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, I_P]
+    L.bert_amd_shard_cuts.restype = ctypes.c_int32
+    L.bert_amd_shard_cuts.argtypes = [ctypes.c_int32, I_P, ctypes.c_int32, I_P]
     L.bert_amd_workspace_rows.restype = ctypes.c_int64
     L.bert_amd_workspace_rows.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     L.bert_amd_last_error.restype = ctypes.c_char_p
@@ -134,6 +138,15 @@ def tokenize_json(tokenizer_json: str, text: str, n_max: int = 512, frame: bool 
     if n < 0:
         raise RuntimeError(last_error())
     return list(buf[:n])
+
+
+def shard_cuts(n_tokens: Sequence[int], n_replicas: int) -> List[int]:
+    """bert_eval_batch's split of a batch over n_replicas devices (no GPU needed)."""
+    nt = np.ascontiguousarray(np.asarray(n_tokens, np.int32))
+    cut = np.zeros(n_replicas + 1, np.int32)
+    if lib().bert_amd_shard_cuts(len(nt), nt.ctypes.data_as(I_P), n_replicas, cut.ctypes.data_as(I_P)) != 0:
+        raise ValueError(last_error())
+    return cut.tolist()
 
 
 def quantize(src: str, dst: str, ftype: str) -> bool:
@@ -288,6 +301,14 @@ class BertModel:
         """bert_amd_set_option (include/bert_amd.h); results are identical under every setting."""
         if self.lib.bert_amd_set_option(self.ctx, key.encode(), int(value)) != 0:
             raise ValueError(f"bert_amd_set_option({key}, {value}) failed: {last_error()}")
+
+    def get_option(self, key: str) -> int:
+        """bert_amd_get_option: a pipeline option, or a resolved load-time choice
+        ("qkva_ntw", "i8_up", "i8_o", "i8_down")."""
+        v = ctypes.c_int32(0)
+        if self.lib.bert_amd_get_option(self.ctx, key.encode(), ctypes.byref(v)) != 0:
+            raise ValueError(f"bert_amd_get_option({key}) failed: {last_error()}")
+        return int(v.value)
 
     def workspace_rows(self, slot: int = 0) -> int:
         return int(self.lib.bert_amd_workspace_rows(self.ctx, slot))

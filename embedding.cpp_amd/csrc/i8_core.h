@@ -8,6 +8,14 @@
 
 namespace bertamd {
 
+// Q4_1 per-block fold order: 1 = ggml's plain-C vec_dot_q4_1_q8_1 exactly
+// (sumf += fmaf(d_w d_a, isum, m_w s_a), in block order), 0 = the m_w s_a
+// terms accumulated two blocks at a time on the f32 MFMA (one fma per output
+// per block).  See DESIGN.md §4 (which ggml build the GPU lands on).
+#ifndef I8_Q41_GENERIC
+#define I8_Q41_GENERIC 0
+#endif
+
 typedef int int4v __attribute__((ext_vector_type(4)));
 typedef int int16v __attribute__((ext_vector_type(16)));
 
@@ -190,6 +198,22 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
     const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
     const float16v zf = {};
     if constexpr (BB < 3) i8_aops<WT, BM, T, BB + 1>(nxt, buf, tt0);
+#if I8_Q41_GENERIC
+    // ggml's plain-C ggml_vec_dot_q4_1_q8_1 per block: sumf += fmaf(d_w d_a,
+    // (float) isum, m_w * s_a) — m_w * s_a rounded on its own (the f32 MFMA with
+    // one nonzero product per output), then one fma and one add per output
+    float16v ms[F][T];
+    if constexpr (WT == W_Q4_1) {
+        const float *sbuf = (const float *)(buf + C::QB + C::DB);
+#pragma unroll
+        for (int t = 0; t < T; t++) {
+            const float sa = sbuf[BB * BM + 32 * (tt0 + t) + l32];
+#pragma unroll
+            for (int f = 0; f < F; f++)
+                ms[f][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh ? 0.f : wm[f][BB], sa, zf, 0, 0, 0);
+        }
+    }
+#else
     if constexpr (WT == W_Q4_1 && (BB & 1)) {
         // m_w * s_a of blocks b - 1 (k = 0, lanes 0-31) and b (k = 1, lanes 32-63)
         const float *sbuf = (const float *)(buf + C::QB + C::DB);
@@ -201,6 +225,7 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
                 acc[f][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh ? wm[f][BB] : wm[f][BB - 1], sa, acc[f][t], 0, 0, 0);
         }
     }
+#endif
     // dd = d_w * d_a, exact: Q4_0 fp16 x fp16 on the f16 MFMA (ws: the f-tile's
     // four block scales at k = 0..3, oh: d_a one-hot at k = BB); Q4_1 f32 x f32
     // on the f32 MFMA
@@ -245,7 +270,15 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 16; i++) {
+#if I8_Q41_GENERIC
+            float v;
+            if constexpr (WT == W_Q4_1)
+                v = acc[p / T][p % T][i] + __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], ms[p / T][p % T][i]);
+            else
+                v = __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], acc[p / T][p % T][i]);
+#else
             float v = __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], acc[p / T][p % T][i]);
+#endif
             asm volatile("" : "+v"(v));  // keep the fold here: sunk past the MFMAs it would keep every tile live
             acc[p / T][p % T][i] = v;
         }

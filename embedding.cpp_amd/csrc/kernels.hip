@@ -1896,7 +1896,8 @@ __global__ __launch_bounds__(ATTN_LONG_NW * 64, ATTN_LONG_OCC(D)) void attention
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
     const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
-    if (n <= NK || qb * ATTN_LONG_QB >= n) return;  // n <= 128: attention_short_kernel
+    // n <= 128 belongs to attention_short_kernel, whatever the chunk size NK
+    if (n <= 128 || qb * ATTN_LONG_QB >= n) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
     const int E = a.E, E2 = 2 * E;
     const bool v_aligned = (beg & 7) == 0;

@@ -257,7 +257,7 @@ struct bert_ctx {
     WordPieceTokenizer tokenizer;
     std::vector<std::unique_ptr<Replica>> reps;
     // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
-    bool i8_o = false, i8_up = false, i8_down = false;
+    bool i8_qkv = false, i8_o = false, i8_down = false, i8_up = false;
     // the fused QKV + attention kernel's form, fixed at load: 1 or 2 = the
     // head-pair kernel with that many 192-feature units per main loop (the tile
     // grouping of its QKV weight copy), 0 = the producer / consumer kernel on an
@@ -297,12 +297,64 @@ bool dmalloc(std::vector<void *> &track, T **p, size_t bytes) {
     return true;
 }
 
-template <typename T>
-bool upload(std::vector<void *> &track, T **p, const void *src, size_t bytes) {
-    if (!dmalloc(track, p, bytes)) return false;
-    HIP_OK(hipMemcpy(*p, src, bytes, hipMemcpyHostToDevice));
-    return true;
-}
+// Weight staging for a load over one or more devices.  The host form of every
+// device weight buffer (repack, repack_i8, table_f32: the costly part of a
+// load) is made ONCE, by a recording pass over build_replica; then one host
+// thread per device replays the same sequence of puts, allocating and copying
+// on its own device, so N replicas cost one repack plus N concurrent uploads
+// (reference bert.cpp:1065-1107: the replicas serve independent sentences).
+struct StageBuf {
+    std::vector<uint8_t> own;  // bytes made by the recording pass
+    const void *ext = nullptr; // or host memory that outlives the load (GGUF data, tables())
+    size_t n = 0;
+    float unscale = 1.f;       // split-fp16 weights' 2^-S (kernels.h WPtr)
+};
+struct Stager {
+    std::vector<StageBuf> *book = nullptr;  // shared; filled while recording, read-only on replay
+    bool replay = false;
+    size_t next = 0;                        // replay cursor (one Stager per replica)
+    std::vector<void *> *track = nullptr;   // replay: the replica's allocations
+    // record: make the bytes; replay: allocate on the current device and copy
+    template <typename T, typename F>
+    bool put(T **p, F make, float *unscale = nullptr) {
+        if (!replay) {
+            StageBuf b;
+            make(b);
+            b.n = b.ext ? b.n : b.own.size();
+            book->push_back(std::move(b));
+            return true;
+        }
+        if (next >= book->size()) {
+            set_err("internal: weight staging replay out of step");
+            return false;
+        }
+        const StageBuf &b = (*book)[next++];
+        if (!dmalloc(*track, p, b.n)) return false;
+        HIP_OK(hipMemcpy(*p, b.ext ? b.ext : b.own.data(), b.n, hipMemcpyHostToDevice));
+        if (unscale) *unscale = b.unscale;
+        return true;
+    }
+    // host memory that stays valid for the whole load: referenced, not copied
+    template <typename T>
+    bool put_ext(T **p, const void *src, size_t bytes) {
+        return put(p, [&](StageBuf &b) {
+            b.ext = src;
+            b.n = bytes;
+        });
+    }
+    // record: bytes of the vector get(*h) (h made once by the caller); replay: h is unused
+    template <typename T, typename H, typename G>
+    bool put_vec_or(T **p, const std::shared_ptr<H> &h, G get) {
+        return put(p, [&](StageBuf &b) {
+            const auto &v = get(*h);
+            b.own.assign((const uint8_t *)v.data(), (const uint8_t *)(v.data() + v.size()));
+        });
+    }
+    template <typename T, typename V>
+    bool put_vec(T **p, const std::vector<V> &v) {  // record: a copy of v's bytes
+        return put(p, [&](StageBuf &b) { b.own.assign((const uint8_t *)v.data(), (const uint8_t *)(v.data() + v.size())); });
+    }
+};
 
 // Repack a [N][K] ggml-format matrix (given as row pointers) into MFMA
 // fragment order (kernels.h WPtr).
@@ -442,11 +494,22 @@ I8Host repack_i8(uint32_t type, const std::vector<const uint8_t *> &rows, int64_
     return h;
 }
 
-bool upload_i8w(std::vector<void *> &track, I8W &w, const I8Host &h) {
+// Repack a Q4_0 / Q4_1 [N][K] matrix for the int8-MFMA GEMMs (kernels.h
+// I8W): nibbles expanded to int8 (q - 8 for Q4_0, q for Q4_1) in fragment
+// order, the fp16 block scales (and Q4_1 minima) widened to f32 vectors.
+// Weight row m of each 32-row tile holds feature perm(m), so that a lane of
+// the 32x32 MFMA result holds 16 consecutive output features.  Staged as up
+// to four buffers (q, d, m, dh); the repack runs once, while recording.
+bool stage_i8(Stager &S, I8W &w, uint32_t type, const std::vector<const uint8_t *> &rows, int64_t K) {
+    std::shared_ptr<I8Host> h;
+    if (!S.replay) h = std::make_shared<I8Host>(repack_i8(type, rows, K));
+    const bool q1 = type == GT_Q4_1;
     void *pq = nullptr, *pd = nullptr, *pm = nullptr, *ph = nullptr;
-    if (!upload(track, &pq, h.q.data(), h.q.size()) || !upload(track, &pd, h.d.data(), h.d.size() * 4)) return false;
-    if (!h.m.empty() && !upload(track, &pm, h.m.data(), h.m.size() * 4)) return false;
-    if (!h.dh.empty() && !upload(track, &ph, h.dh.data(), h.dh.size() * 2)) return false;
+    if (!S.put_vec_or(&pq, h, [](const I8Host &x) -> const auto & { return x.q; }) ||
+        !S.put_vec_or(&pd, h, [](const I8Host &x) -> const auto & { return x.d; }))
+        return false;
+    if (q1 && !S.put_vec_or(&pm, h, [](const I8Host &x) -> const auto & { return x.m; })) return false;
+    if (!q1 && !S.put_vec_or(&ph, h, [](const I8Host &x) -> const auto & { return x.dh; })) return false;
     w.q = (const int8_t *)pq;
     w.d = (const float *)pd;
     w.m = (const float *)pm;
@@ -454,21 +517,20 @@ bool upload_i8w(std::vector<void *> &track, I8W &w, const I8Host &h) {
     return true;
 }
 
-// Repack a Q4_0 / Q4_1 [N][K] matrix for the int8-MFMA GEMMs (kernels.h
-// I8W): nibbles expanded to int8 (q - 8 for Q4_0, q for Q4_1) in fragment
-// order, the fp16 block scales (and Q4_1 minima) widened to f32 vectors.
-// Weight row m of each 32-row tile holds feature perm(m), so that a lane of
-// the 32x32 MFMA result holds 16 consecutive output features.
-bool upload_i8(std::vector<void *> &track, I8W &w, uint32_t type, const std::vector<const uint8_t *> &rows,
-               int64_t K) {
-    return upload_i8w(track, w, repack_i8(type, rows, K));
-}
-
-bool upload_packed(std::vector<void *> &track, WPtr &w, const Packed &p) {
+// A split-fp16 / f16 / f32 weight matrix in MFMA fragment order (repack, run
+// once while recording).
+template <typename F>
+bool stage_packed(Stager &S, WPtr &w, F make_packed) {
     void *q = nullptr;
-    if (!upload(track, &q, p.q.data(), p.q.size())) return false;
+    float unscale = 1.f;
+    if (!S.put(&q, [&](StageBuf &b) {
+            Packed p = make_packed();
+            b.own = std::move(p.q);
+            b.unscale = p.unscale;
+        }, &unscale))
+        return false;
     w.q = q;
-    w.unscale = p.unscale;
+    w.unscale = unscale;
     return true;
 }
 
@@ -623,6 +685,11 @@ void i8_select(bert_ctx *ctx, const std::string &spec) {
         const std::string t = std::string(",") + v + ",";
         return all || t.find(std::string(",") + p + ",") != std::string::npos;
     };
+    // qkv: the unfused QKV GEMM on the int8 copy (as the producer / consumer
+    // kernel's twin); the head-pair fused kernel has no int8 form, so a model
+    // that would use it runs every batch on the unfused pair instead (the
+    // results of a sentence must not depend on its batch)
+    ctx->i8_qkv = q4 && (ctx->qkva_ntw == 0 || has("qkv")) && i8_gemm_supported(EPI_QKV, 3 * E, E);
     ctx->i8_up = q4 && has("up") && i8_gemm_supported(EPI_GELU_ACT, I, E);
     ctx->i8_o = q4 && has("o") && i8_gemm_supported(ln, E, E);
     ctx->i8_down = q4 && has("down") && i8_gemm_supported(ln, E, I);
@@ -675,7 +742,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
             qf.Wi = L.qkv8;  // (qkva_ntw 0)
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
-        } else if (ctx->qkva_ntw == 0) {  // the int8 QKV of the producer / consumer kernel, unfused
+        } else if (ctx->i8_qkv) {  // the int8 QKV of the producer / consumer kernel, unfused
             q.Wi = L.qkv8;
             LAUNCH_OK("gemm_qkv", launch_gemm_i8(wt, EPI_QKV, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
@@ -804,8 +871,10 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
     const bool ln_fused = gemm_ln_fused(wt, E);
     // QKV + attention in one kernel when every sentence fits one 128-row tile
     // (option "unfused" forces the two-kernel path, for A/B checks)
-    const bool fused_qkv_attn =
-        !ctx->unfused && n_seqs >= ctx->fuse_min && qkv_attention_supported(wt, E, H, max_len, ctx->qkva_ntw);
+    // (an int8 QKV copy without the producer / consumer kernel, i8 qkv: the
+    // head-pair kernel has no int8 form, so every batch takes the unfused pair)
+    const bool fused_qkv_attn = !ctx->unfused && n_seqs >= ctx->fuse_min && (!ctx->i8_qkv || ctx->qkva_ntw == 0) &&
+                                qkv_attention_supported(wt, E, H, max_len, ctx->qkva_ntw);
 
     const EmbedArgs ea = embed_args(ctx, R, w, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(ctx->wtype, ea, (int)Mpad, st));
@@ -999,20 +1068,28 @@ bool add_lane(Replica &R) {
     return true;
 }
 
-bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
-    R.device = device;
-    HIP_OK(hipSetDevice(device));
-    if (!add_lane(R)) return false;
-    auto &tr = R.weight_allocs;
-    const std::vector<float> word = table_f32(hm.word), pos = table_f32(hm.pos), type = table_f32(hm.type);
-    if (!upload(tr, &R.word, word.data(), word.size() * 4) || !upload(tr, &R.pos, pos.data(), pos.size() * 4) ||
-        !upload(tr, &R.type, type.data(), type.size() * 4) ||
-        !upload(tr, &R.ln_e_w, hm.ln_e_w->data, hm.ln_e_w->nbytes) ||
-        !upload(tr, &R.ln_e_b, hm.ln_e_b->data, hm.ln_e_b->nbytes) ||
-        !upload(tr, &R.gelu_tab, tables().gelu.data(), 65536 * 2) ||
-        !upload(tr, &R.exp_tab, tables().expt.data(), 65536 * 2) ||
-        !upload(tr, &R.gelu_compact, tables().gelu_pair.data(), tables().gelu_pair.size() * 2) ||
-        !upload(tr, &R.exp_compact, tables().exp_c.compact.data(), tables().exp_c.compact.size() * 2))
+// The device form of a model, as a sequence of staged buffers: with
+// S.replay false it only makes the host bytes (no device call); with S.replay
+// true it allocates and uploads them on R.device, in the same order.
+bool build_replica(bert_ctx *ctx, const HostModel &hm, Stager &S, Replica &R) {
+    if (S.replay) {
+        HIP_OK(hipSetDevice(R.device));
+        if (!add_lane(R)) return false;
+        S.track = &R.weight_allocs;
+    }
+    auto table = [&](void **p, const GGUFTensor *t) {
+        return S.put(p, [&](StageBuf &b) {
+            const std::vector<float> v = table_f32(t);
+            b.own.assign((const uint8_t *)v.data(), (const uint8_t *)(v.data() + v.size()));
+        });
+    };
+    if (!table(&R.word, hm.word) || !table(&R.pos, hm.pos) || !table(&R.type, hm.type) ||
+        !S.put_ext(&R.ln_e_w, hm.ln_e_w->data, hm.ln_e_w->nbytes) ||
+        !S.put_ext(&R.ln_e_b, hm.ln_e_b->data, hm.ln_e_b->nbytes) ||
+        !S.put_ext(&R.gelu_tab, tables().gelu.data(), 65536 * 2) ||
+        !S.put_ext(&R.exp_tab, tables().expt.data(), 65536 * 2) ||
+        !S.put_ext(&R.gelu_compact, tables().gelu_pair.data(), tables().gelu_pair.size() * 2) ||
+        !S.put_ext(&R.exp_compact, tables().exp_c.compact.data(), tables().exp_c.compact.size() * 2))
         return false;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const uint32_t wt = hm.layers[0].q_w->type;
@@ -1032,9 +1109,10 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                     const GGUFTensor *bt = part == 0 ? l.q_b : part == 1 ? l.k_b : l.v_b;
                     bqkv[dst] = ((const float *)bt->data)[src];
                 }
-        if (ctx->qkva_ntw == 0) {
-            // producer / consumer kernel and its unfused twin: int8 codes, head-major f-tiles
-            if (!upload_i8(tr, dl.qkv8, wt, rows, E)) return false;
+        if (ctx->i8_qkv) {
+            // producer / consumer kernel and its unfused twin (or the unfused
+            // int8 QKV GEMM alone, i8 qkv): int8 codes, head-major f-tiles
+            if (!stage_i8(S, dl.qkv8, wt, rows, E)) return false;
         } else if (qkv_attention_supported(ctx->wtype, (int)E, (int)ctx->hp.n_head, 128, ctx->qkva_ntw)) {
             // undo repack's column interleave (row 32p + 2c + t <- 32p + 16t + c) so
             // that repacked tile j holds features 16j .. 16j + 15 in order
@@ -1051,7 +1129,7 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
             for (size_t pr = 0; pr < rows.size() / 32; pr++)
                 for (int t = 0; t < 2; t++)
                     for (int c = 0; c < 16; c++) plain[32 * pr + 2 * c + t] = quad[32 * pr + 16 * t + c];
-            if (!upload_packed(tr, dl.qkv_plain, repack(wt, plain, E))) return false;
+            if (!stage_packed(S, dl.qkv_plain, [&] { return repack(wt, plain, E); })) return false;
         }
         std::vector<const uint8_t *> up_rows = rows_of(l.i_w);
         if (gemm_gelu_blk8(ctx->wtype)) {
@@ -1063,21 +1141,23 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, int device, Replica &R) {
                 for (int t = 0; t < 2; t++)
                     for (int r = 0; r < 16; r++) up_rows[32 * pr + 2 * r + t] = src[32 * pr + 8 * (r >> 2) + 4 * t + (r & 3)];
         }
-        if (ctx->qkva_ntw != 0 && !upload_packed(tr, dl.qkv, repack(wt, rows, E))) return false;
+        if (!ctx->i8_qkv && !stage_packed(S, dl.qkv, [&] { return repack(wt, rows, E); })) return false;
         // each projection in the one format its GEMM reads (int8 or split fp16)
-        if (!(ctx->i8_o ? upload_i8(tr, dl.o8, wt, rows_of(l.o_w), E) : upload_packed(tr, dl.o, repack(wt, rows_of(l.o_w), E))) ||
-            !(ctx->i8_up ? upload_i8(tr, dl.up8, wt, rows_of(l.i_w), E) : upload_packed(tr, dl.up, repack(wt, up_rows, E))) ||
-            !(ctx->i8_down ? upload_i8(tr, dl.down8, wt, rows_of(l.o2_w), I)
-                           : upload_packed(tr, dl.down, repack(wt, rows_of(l.o2_w), I))))
+        if (!(ctx->i8_o ? stage_i8(S, dl.o8, wt, rows_of(l.o_w), E)
+                        : stage_packed(S, dl.o, [&] { return repack(wt, rows_of(l.o_w), E); })) ||
+            !(ctx->i8_up ? stage_i8(S, dl.up8, wt, rows_of(l.i_w), E)
+                         : stage_packed(S, dl.up, [&] { return repack(wt, up_rows, E); })) ||
+            !(ctx->i8_down ? stage_i8(S, dl.down8, wt, rows_of(l.o2_w), I)
+                           : stage_packed(S, dl.down, [&] { return repack(wt, rows_of(l.o2_w), I); })))
             return false;
-        if (!upload(tr, &dl.b_qkv, bqkv.data(), bqkv.size() * 4) || !upload(tr, &dl.b_o, l.o_b->data, E * 4) ||
-            !upload(tr, &dl.b_up, l.i_b->data, I * 4) || !upload(tr, &dl.b_down, l.o2_b->data, E * 4) ||
-            !upload(tr, &dl.ln1_w, l.ln1_w->data, E * 4) || !upload(tr, &dl.ln1_b, l.ln1_b->data, E * 4) ||
-            !upload(tr, &dl.ln2_w, l.ln2_w->data, E * 4) || !upload(tr, &dl.ln2_b, l.ln2_b->data, E * 4))
+        if (!S.put_vec(&dl.b_qkv, bqkv) || !S.put_ext(&dl.b_o, l.o_b->data, E * 4) ||
+            !S.put_ext(&dl.b_up, l.i_b->data, I * 4) || !S.put_ext(&dl.b_down, l.o2_b->data, E * 4) ||
+            !S.put_ext(&dl.ln1_w, l.ln1_w->data, E * 4) || !S.put_ext(&dl.ln1_b, l.ln1_b->data, E * 4) ||
+            !S.put_ext(&dl.ln2_w, l.ln2_w->data, E * 4) || !S.put_ext(&dl.ln2_b, l.ln2_b->data, E * 4))
             return false;
         R.L.push_back(dl);
     }
-    HIP_OK(hipDeviceSynchronize());
+    if (S.replay) HIP_OK(hipDeviceSynchronize());
     return true;
 }
 
@@ -1183,6 +1263,10 @@ bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
         const long v = std::strtol(p.second.c_str(), &end, 10);
         if (p.second.empty() || *end) {
             set_err("bert_amd option %s: '%s' is not an integer", p.first.c_str(), p.second.c_str());
+            return false;
+        }
+        if (v < INT32_MIN || v > INT32_MAX) {  // no silent wrap when narrowing to int32
+            set_err("bert_amd option %s: '%s' is out of the int32 range", p.first.c_str(), p.second.c_str());
             return false;
         }
         if (p.first == "qkva_ntw") {
@@ -1319,7 +1403,6 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     }
     std::string i8_spec;
     if (!parse_load_options(ctx.get(), opts, i8_spec)) return nullptr;
-    i8_select(ctx.get(), i8_spec);
     // the producer / consumer fused kernel exists for Q4_0 at head dim 32, n_embd
     // 384 (MiniLM; measured +1.2% batch-1024, +6% ragged over the head-pair
     // kernel): auto takes it there and the 2-unit head-pair kernel
@@ -1328,6 +1411,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
     const bool pc_ok = qkv_attention_supported(ctx->wtype, (int)E, hp.n_head, 128, 0);
     if (ctx->qkva_ntw < 0) ctx->qkva_ntw = pc_ok ? 0 : 2;
     if (ctx->qkva_ntw == 0 && !pc_ok) ctx->qkva_ntw = 1;
+    i8_select(ctx.get(), i8_spec);
     // devices
     int n_visible = 0;
     if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) {
@@ -1342,15 +1426,44 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
         devs = parse_device_env(n_visible);
     }
     if (devs.empty()) { set_err("no usable device in the requested list"); return nullptr; }
+    // the host forms of every weight buffer, made once (Stager), then one
+    // upload thread per replica
+    std::vector<StageBuf> book;
+    {
+        Stager rec;
+        rec.book = &book;
+        Replica scratch;
+        if (!build_replica(ctx.get(), hm, rec, scratch)) return nullptr;
+    }
     for (int d : devs) {
-        auto R = std::make_unique<Replica>();
-        if (!build_replica(ctx.get(), hm, d, *R)) {
-            free_replica(*R);
+        ctx->reps.push_back(std::make_unique<Replica>());
+        ctx->reps.back()->device = d;
+    }
+    std::vector<std::string> errs(devs.size());
+    {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < devs.size(); i++)
+            th.emplace_back([&, i] {
+                try {
+                    Stager up;
+                    up.book = &book;
+                    up.replay = true;
+                    if (!build_replica(ctx.get(), hm, up, *ctx->reps[i]) ) errs[i] = g_err;
+                    else if (up.next != book.size()) errs[i] = "internal: weight staging replay out of step";
+                } catch (const std::exception &e) {
+                    errs[i] = e.what();
+                } catch (...) {
+                    errs[i] = "unknown exception";
+                }
+            });
+        for (auto &t : th) t.join();
+    }
+    for (size_t i = 0; i < devs.size(); i++)
+        if (!errs[i].empty()) {
+            set_err("device %d: %s", devs[i], errs[i].c_str());
             for (auto &r : ctx->reps) free_replica(*r);
             return nullptr;
         }
-        ctx->reps.push_back(std::move(R));
-    }
     std::printf("%s: n_vocab = %d, n_max_tokens = %d, n_embd = %d, n_intermediate = %d, n_head = %d, n_layer = %d, "
                 "weights = %s, devices = %zu\n",
                 "bert_load_from_file", hp.n_vocab, hp.n_max_tokens, hp.n_embd, hp.n_intermediate, hp.n_head,
@@ -1594,23 +1707,29 @@ void eval_batch_impl(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *nt
     });
 }
 
-// Shards one ragged batch over the context's replicas (caller holds ctx->mu).
-void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
-    const int nr = (int)ctx->reps.size();
-    // contiguous slices balanced by token count
-    std::vector<int> cut(nr + 1, n);
+// Contiguous slices of a batch for nr replicas, balanced by token count:
+// cut[0] = 0 <= cut[1] <= ... <= cut[nr] = n, slice r = [cut[r], cut[r+1]).
+// Slice r ends at the first sentence where the running token count reaches
+// r+1 nr-ths of the total, so every slice holds at most total/nr + one
+// sentence's tokens (tests/test_abi.py::test_shard_cuts_balance_and_cover).
+void shard_cuts(int32_t n, const int32_t *ntok, int nr, int32_t *cut) {
+    for (int r = 0; r <= nr; r++) cut[r] = n;
     cut[0] = 0;
     int64_t total = 0;
     for (int s = 0; s < n; s++) total += ntok[s];
-    {
-        int64_t acc = 0;
-        int r = 1;
-        for (int s = 0; s < n && r < nr; s++) {
-            acc += ntok[s];
-            while (r < nr && acc * nr >= total * r) cut[r++] = s + 1;
-        }
-        for (; r < nr; r++) cut[r] = n;
+    int64_t acc = 0;
+    int r = 1;
+    for (int s = 0; s < n && r < nr; s++) {
+        acc += ntok[s];
+        while (r < nr && acc * nr >= total * r) cut[r++] = s + 1;
     }
+}
+
+// Shards one ragged batch over the context's replicas (caller holds ctx->mu).
+void dispatch_batch(bert_ctx *ctx, int32_t n, bert_vocab_id **toks, int32_t *ntok, float **embs) {
+    const int nr = (int)ctx->reps.size();
+    std::vector<int> cut(nr + 1);
+    shard_cuts(n, ntok, nr, cut.data());
     if (nr == 1) {
         if (!eval_host_slice(ctx, *ctx->reps[0], *ctx->reps[0]->lanes[0], toks, ntok, embs, 0, n))
             std::fprintf(stderr, "bert_eval_batch: %s\n", g_err.c_str());
@@ -2051,6 +2170,36 @@ int32_t bert_amd_set_option(bert_ctx *ctx, const char *key, int32_t value) {
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
     return apply_option(ctx, key, value);
+}
+
+int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
+    if (!ctx || !key || !value) {
+        set_err("bert_amd_get_option: invalid arguments");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const std::string k = key;
+    const std::pair<const char *, int32_t> opts[] = {
+        {"split", ctx->split}, {"pack", ctx->pack}, {"fuse_min", ctx->fuse_min}, {"unfused", ctx->unfused},
+        {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
+        {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
+        {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down}};
+    for (const auto &o : opts)
+        if (k == o.first) {
+            *value = o.second;
+            return 0;
+        }
+    set_err("bert_amd_get_option: unknown option '%s'", key);
+    return -2;
+}
+
+int32_t bert_amd_shard_cuts(int32_t n_seqs, const int32_t *n_tokens, int32_t n_replicas, int32_t *cut) {
+    if (n_seqs < 0 || (n_seqs > 0 && !n_tokens) || n_replicas <= 0 || !cut) {
+        set_err("bert_amd_shard_cuts: invalid arguments");
+        return -1;
+    }
+    shard_cuts(n_seqs, n_tokens, n_replicas, cut);
+    return 0;
 }
 
 int64_t bert_amd_workspace_rows(bert_ctx *ctx, int32_t slot) {

@@ -136,6 +136,20 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
    Results are identical under every setting. */
 BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int32_t value);
 
+/* Reads an option back into *value: every bert_amd_set_option key, plus the
+   load-time choices as resolved for this model — "qkva_ntw" (0, 1 or 2) and
+   "i8_up", "i8_o", "i8_down" (1 when that Q4 projection runs on the
+   int8-MFMA GEMMs).  Lets bench.py price each kernel on the arithmetic it
+   runs.  Returns 0, or -2 on an unknown key. */
+BERT_API int32_t bert_amd_get_option(struct bert_ctx *ctx, const char *key, int32_t *value);
+
+/* How bert_eval_batch splits a batch over n_replicas devices: contiguous
+   sentence slices balanced by token count, slice r = [cut[r], cut[r+1]),
+   cut[0] = 0, cut[n_replicas] = n_seqs (cut has n_replicas + 1 entries).
+   Pure host function (no device needed); lets tests check balance and
+   coverage.  Returns 0, or -1 on invalid arguments. */
+BERT_API int32_t bert_amd_shard_cuts(int32_t n_seqs, const int32_t *n_tokens, int32_t n_replicas, int32_t *cut);
+
 BERT_API const char *bert_amd_last_error(void);
 
 #ifdef __cplusplus

@@ -11,7 +11,11 @@ before comparing.  The reference itself cannot be built or run here
 oracle is pinned separately (tests/test_oracle.py).
 
 Run:  python tests/golden/make_golden.py [case ...]
-      python tests/golden/make_golden.py --spread [case ...]   (only add the ggml-order spread)
+      python tests/golden/make_golden.py --spread [case ...]   (only add the ggml-order variants and spread)
+
+Each fixture also holds the oracle's embeddings under ggml's other build orders
+(emb_generic: the plain-C fallback, emb_lanes16: the AVX-512 width), so the GPU
+tests can report and pin how close the GPU lands to each named build.
 """
 from __future__ import annotations
 
@@ -105,36 +109,59 @@ def load_case(name: str):
     return meta, toks, z["emb"]
 
 
-def order_spread(path: str, toks, emb) -> list[float]:
-    """Per sentence, the largest 1 - cos between the AVX2 oracle (`emb`) and
-    the same semantics under the other summation orders ggml@8ca2c19 builds
-    use (oracle.DOT_VARIANTS: plain-C fallback, 16-lane width): how far two
-    valid ggml CPU runs of the reference land apart on this input."""
+def order_variants(path: str, toks) -> dict:
+    """The oracle's embeddings under ggml's other summation orders
+    (oracle.DOT_VARIANTS except the AVX2 checker: plain-C fallback, 16-lane
+    width) — what two other valid ggml CPU builds of the reference output."""
     import oracle
     o = oracle.Oracle(path)
-    worst = np.zeros(len(toks))
+    out = {}
     try:
         for v in oracle.DOT_VARIANTS:
             if v == "avx2":
                 continue
             oracle.set_dot_variant(v)
-            a = o.eval_batch(toks, 0).astype(np.float64)
-            c = (a * emb).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(emb, axis=1)
-            worst = np.maximum(worst, 1 - c)
+            out[v] = o.eval_batch(toks, 0).astype(np.float32)
     finally:
         oracle.set_dot_variant("avx2")
+    return out
+
+
+def order_spread(variants: dict, emb) -> list[float]:
+    """Per sentence, the largest 1 - cos between the AVX2 oracle (`emb`) and
+    the same semantics under the other summation orders ggml@8ca2c19 builds
+    use: how far two valid ggml CPU runs of the reference land apart on this
+    input."""
+    emb = np.asarray(emb, np.float64)
+    worst = np.zeros(len(emb))
+    for a in variants.values():
+        a = a.astype(np.float64)
+        c = (a * emb).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(emb, axis=1)
+        worst = np.maximum(worst, 1 - c)
     return [float(x) for x in worst]
 
 
+def save(name: str, tokens, offsets, emb, meta: dict, variants: dict):
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), tokens=tokens, offsets=offsets, emb=emb,
+                        meta=np.array(json.dumps(meta)), **{f"emb_{k}": v for k, v in variants.items()})
+
+
+def load_variants(name: str) -> dict:
+    """The fixture's embeddings under ggml's other build orders: {"generic": .., "lanes16": ..}."""
+    z = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+    return {k[4:]: z[k] for k in z.files if k.startswith("emb_")}
+
+
 def add_spread(name: str, model_dir: str):
-    """Add ggml_order_spread_1mcos to an existing fixture (inputs/outputs unchanged)."""
+    """Add the variant embeddings and ggml_order_spread_1mcos to an existing
+    fixture (inputs/outputs unchanged)."""
     meta, toks, emb = load_case(name)
     path = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
     assert sha256(path) == meta["model_sha256"]
-    meta["ggml_order_spread_1mcos"] = order_spread(path, toks, emb.astype(np.float64))
+    var = order_variants(path, toks)
+    meta["ggml_order_spread_1mcos"] = order_spread(var, emb)
     z = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
-    np.savez_compressed(os.path.join(HERE, name + ".npz"), tokens=z["tokens"], offsets=z["offsets"], emb=z["emb"],
-                        meta=np.array(json.dumps(meta)))
+    save(name, z["tokens"], z["offsets"], z["emb"], meta, var)
     print(f"{name}: ggml order spread {meta['ggml_order_spread_1mcos']}", flush=True)
 
 
@@ -156,7 +183,8 @@ def make(name: str, model_dir: str):
     meta = dict(case=name, shape=shape, hparams=hp, ftype=ftype, seed=SEED, w_std=w_std, lengths=lens,
                 n_layer=n_layer, model_sha256=sha256(path), oracle_seconds=round(dt, 2),
                 generator="bertlib.synth_model (csrc/synth.cpp)", oracle="oracle/bert_oracle.c")
-    meta["ggml_order_spread_1mcos"] = order_spread(path, toks, emb)
+    var = order_variants(path, toks)
+    meta["ggml_order_spread_1mcos"] = order_spread(var, emb)
     if name in CHAOTIC:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import numpy_ref
@@ -164,8 +192,7 @@ def make(name: str, model_dir: str):
         ex = np.stack([m.eval(t) for t in toks]).astype(np.float64)
         c = (ex * emb).sum(1) / np.linalg.norm(ex, axis=1) / np.linalg.norm(emb, axis=1)
         meta["exact_restatement_1mcos"] = [float(1 - v) for v in c]
-    np.savez_compressed(os.path.join(HERE, name + ".npz"), tokens=np.concatenate(toks).astype(np.int32),
-                        offsets=offs, emb=emb.astype(np.float32), meta=np.array(json.dumps(meta)))
+    save(name, np.concatenate(toks).astype(np.int32), offs, emb.astype(np.float32), meta, var)
     print(f"{name}: {len(toks)} sentences, oracle {dt:.1f}s", flush=True)
 
 

@@ -161,3 +161,30 @@ def test_reference_consumers_compile_unchanged(repo, tmp_path):
                             os.path.join(REF, "examples", ex), "-o", str(out), "-L", os.path.join(repo, "build"),
                             "-lbert", "-Wl,-rpath," + os.path.join(repo, "build")], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("n_rep", [1, 2, 3, 8])
+def test_shard_cuts_balance_and_cover(n_rep):
+    """bert_eval_batch's split over replicas (runtime.cpp shard_cuts, reference
+    bert.cpp:1065-1107: sentences are independent): contiguous slices that
+    cover the batch exactly once, in order, each within one sentence of the
+    token-balanced share — on the shape bert_encode_batch hands it (lengths
+    sorted ascending, bert.cpp:1163-1196), on uniform and on ragged batches,
+    and when there are fewer sentences than replicas."""
+    rng = np.random.default_rng(n_rep)
+    cases = [np.sort(rng.integers(1, 513, 4096)), np.full(1024, 128), rng.integers(1, 129, 777),
+             np.sort(rng.integers(2, 41, 300)), np.array([512, 1, 1, 1]), np.array([5]), np.array([], np.int64)]
+    for lens in cases:
+        cut = bertlib.shard_cuts(lens, n_rep)
+        assert len(cut) == n_rep + 1 and cut[0] == 0 and cut[-1] == len(lens)
+        assert all(a <= b for a, b in zip(cut, cut[1:]))
+        total = int(lens.sum())
+        mx = int(lens.max()) if len(lens) else 0
+        for r in range(n_rep):
+            share = int(lens[cut[r]:cut[r + 1]].sum())
+            assert share <= total / n_rep + mx, (r, share, total / n_rep, mx)
+            # no replica is left idle while another holds more than a share plus one sentence
+        if len(lens) >= n_rep and total >= n_rep * mx:
+            assert all(cut[r + 1] > cut[r] for r in range(n_rep)), cut
+    with pytest.raises(ValueError):
+        bertlib.shard_cuts([1, 2], 0)

@@ -53,6 +53,7 @@ def max_ulp(a, b):
 # attention kernel (fuse_min 0: a 4-sentence batch would otherwise take the
 # unfused pair), C2 F16, and the 24-layer C5 whose 1 - cos 1.75e-3 this explains
 CASES = [
+    ("c5_bge_q4_1", [0], {"i8": "all"}),
     ("c3_minilm_q4_0", [0, 1], {"fuse_min": 0}),
     ("c3_minilm_q4_0", [0], {"fuse_min": 1000}),
     ("c2_minilm_f16", [0], {"fuse_min": 0}),
@@ -61,8 +62,11 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("case,sents,opts", CASES, ids=[f"{c[0]}-{'fused' if c[2].get('fuse_min') == 0 else 'pair'}"
-                                                         for c in CASES])
+def _tag(c):
+    return c[0] + ("-i8all" if c[2].get("i8") == "all" else "-fused" if c[2].get("fuse_min") == 0 else "-pair")
+
+
+@pytest.mark.parametrize("case,sents,opts", CASES, ids=[_tag(c) for c in CASES])
 def test_layer_by_layer_parity(case, sents, opts, model_dir):
     import oracle
     meta, toks, want = load_case(case)
@@ -110,10 +114,12 @@ def test_layer_by_layer_parity(case, sents, opts, model_dir):
                     finally:
                         oracle.set_dot_variant("avx2")
                     spreads.append((1 - cos_rows(alt, loc), max_ulp(alt, loc)))
+                    # the GPU's own layer against that build's layer on the same input
+                    row[f"local_{var}_1mcos"] = 1 - cos_rows(g, alt)
                 row["spread_1mcos"] = max(sp[0] for sp in spreads)
                 row["spread_ulp"] = max(sp[1] for sp in spreads)
             rows.append(row)
-    tag = case + ("-fused" if opts.get("fuse_min") == 0 else "")
+    tag = _tag((case, sents, opts))
     print(f"\n{tag}: stage, chained ulp / 1-cos, local ulp / 1-cos, ggml spread ulp / 1-cos, code mismatches")
     for r in rows:
         print(f"  s{r['sentence']} stage {r['stage']:2d}: {r['chained_ulp']:>10d} {r['chained_1mcos']:.2e} | "
@@ -137,5 +143,9 @@ def test_layer_by_layer_parity(case, sents, opts, model_dir):
     loc = [r["local_1mcos"] for r in rows if r["stage"]]
     spr = [r["spread_1mcos"] for r in rows if r["stage"]]
     print(f"mean local 1-cos {np.mean(loc):.2e}, mean ggml spread {np.mean(spr):.2e}, max local {max(loc):.2e}")
+    for var in ("generic", "lanes16"):
+        lv = [r[f"local_{var}_1mcos"] for r in rows if r["stage"]]
+        print(f"  mean local 1-cos vs the {var} build {np.mean(lv):.2e} (max {max(lv):.2e}, "
+              f"layers where the GPU equals it bit for bit: {sum(v == 0.0 for v in lv)} of {len(lv)})")
     assert max(loc) <= 1e-5, loc
     assert np.mean(loc) <= max(4 * np.mean(spr), 2e-7), (np.mean(loc), np.mean(spr))

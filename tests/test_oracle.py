@@ -144,11 +144,17 @@ def test_ggml_order_spread_reproduces(case, model_dir):
     and 16-lane builds land from its AVX2 build on the fixture's inputs; the
     GPU parity bound of tests/test_gpu_parity.py parity_bound) is reproduced
     by the oracle's alternate summation orders, and the default order is
-    still the AVX2 checker."""
-    from make_golden import order_spread
+    still the AVX2 checker; the variant embeddings stored in the fixture
+    (emb_generic, emb_lanes16) are the variants' outputs, bit for bit."""
+    from make_golden import load_variants, order_spread, order_variants
     meta, toks, want = load_case(case)
     p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
-    got = order_spread(p, toks, want.astype(np.float64))
+    var = order_variants(p, toks)
+    stored = load_variants(case)
+    assert set(stored) == set(var) == {"generic", "lanes16"}
+    for k in var:
+        assert np.array_equal(var[k], stored[k]), k
+    got = order_spread(var, want)
     np.testing.assert_allclose(got, meta["ggml_order_spread_1mcos"], rtol=1e-9, atol=1e-15)
     assert np.array_equal(oracle.Oracle(p).eval_batch(toks, 0), want)
     assert max(got) > 0.0  # the orders really differ

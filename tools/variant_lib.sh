@@ -16,4 +16,6 @@ wait
 HOST=$(ls build/obj/*.o | grep -v -E '/(kernels|gemm_i8)\.o$')
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libbert.so" $HOST "$OUT/kernels.o" "$OUT/gemm_i8.o" -lpthread
 cp build/BUILD_INFO "$OUT/BUILD_INFO" 2>/dev/null || true
+# a variant is not the clean HEAD build: say which one it is
+printf ' variant=%s (%s)' "$NAME" "$FLAGS" >> "$OUT/BUILD_INFO"
 echo "$OUT/libbert.so ($FLAGS)"
