@@ -135,6 +135,10 @@ __device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ 
                        // register budget and is still faster (FFN-down 299 -> 285 us, A/B)
 #endif
 
+#ifndef I8_LN_PIPE
+#define I8_LN_PIPE 1  // i8_block's two-tile software pipeline in this kernel's main loop
+#endif
+
 template <int WT, bool OV = I8_LN_OV>
 __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles) {
     constexpr int NT = 768, BM = 64, F = 1, T = 2, NCOL = 384, NWV = 12;
@@ -188,9 +192,10 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
                     dma_in(xin, k);
                 }
             };
-            i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc, hook);
+            i8_mainloop<WT, NT, BM, F, T, I8_LN_PIPE, decltype(hook), I8_LN_AHEAD>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc,
+                                                                                   hook);
         } else {
-            i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc);
+            i8_mainloop<WT, NT, BM, F, T, I8_LN_PIPE, I8NoHook, I8_LN_AHEAD>(g, m0, ft0, 0, m0n, ft0, smem, pp, acc);
         }
         STAMP(it, 1, NWV);
         if constexpr (!OV) {  // residual tile -> xs

@@ -84,6 +84,8 @@ enum Epi : int {
 constexpr int HALF_TABLE_LDS = 36864;  // max compact GELU entries (72 KiB of LDS)
 constexpr int EXP_TABLE_LDS = 20480;   // max compact exp entries (40 KiB of LDS)
 constexpr int GELU_FLAT_LDS = 50480;  // Q4 FFN-up GEMM: GELU entries [0, 0x8000 + neg_n] (98.6 KiB of LDS)
+// qkv_attention_pc_kernel's exp table: magnitudes [lo_run, neg_n] only (32.5 KiB of LDS)
+constexpr int EXP_PC_LDS = 16640;
 struct HalfTable {
     const uint16_t *full = nullptr;
     const uint16_t *compact = nullptr;  // n_pad entries, n_pad % 8 == 0
@@ -91,6 +93,10 @@ struct HalfTable {
     int pos_identity = 0;
     uint32_t neg_const = 0;
     int cap = 0;  // GELU pair view: compact holds (cap + 1) x {table[m], table[0x8000 | m]}
+    // exp: every magnitude m <= lo_run has the value of magnitude 0 (fp16
+    // exp(-x) rounds to 1.0 for x < 2^-12), so a lookup may clamp m to
+    // [lo_run, neg_n] and read compact[pos_n + lo_run ..] only
+    int lo_run = 0;
 };
 
 struct GemmArgs {
