@@ -84,8 +84,6 @@ enum Epi : int {
 constexpr int HALF_TABLE_LDS = 36864;  // max compact GELU entries (72 KiB of LDS)
 constexpr int EXP_TABLE_LDS = 20480;   // max compact exp entries (40 KiB of LDS)
 constexpr int GELU_FLAT_LDS = 50480;  // Q4 FFN-up GEMM: GELU entries [0, 0x8000 + neg_n] (98.6 KiB of LDS)
-// qkv_attention_pc_kernel's exp table: magnitudes [lo_run, neg_n] only (32.5 KiB of LDS)
-constexpr int EXP_PC_LDS = 16640;
 struct HalfTable {
     const uint16_t *full = nullptr;
     const uint16_t *compact = nullptr;  // n_pad entries, n_pad % 8 == 0
@@ -93,10 +91,6 @@ struct HalfTable {
     int pos_identity = 0;
     uint32_t neg_const = 0;
     int cap = 0;  // GELU pair view: compact holds (cap + 1) x {table[m], table[0x8000 | m]}
-    // exp: every magnitude m <= lo_run has the value of magnitude 0 (fp16
-    // exp(-x) rounds to 1.0 for x < 2^-12), so a lookup may clamp m to
-    // [lo_run, neg_n] and read compact[pos_n + lo_run ..] only
-    int lo_run = 0;
 };
 
 struct GemmArgs {
@@ -186,6 +180,9 @@ bool gemm_gelu_blk8(int wtype);
 // EPI_LN (N == 384), EPI_RESID (N % 256 == 0), EPI_QKV (N % 384 == 0; the
 // head-major QKV weights of qkv_attention_pc_kernel); K % 128 == 0; Mpad % 128 == 0.
 bool i8_gemm_supported(int epi, int N, int K);
+#ifdef PHASE_STAMPS
+hipError_t stamps_set(unsigned long long *buf, int nblk);  // development stamp builds (kernels.hip)
+#endif
 hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
 
 }  // namespace bertamd

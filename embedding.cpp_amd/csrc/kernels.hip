@@ -1557,58 +1557,37 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 // into the head's attention tiles.  Waves 6-9 consume: query block w - 6 of
 // the head finished in the previous period — the attention task of
 // qkv_attention_kernel.  Period p overlaps head p's projection with head
-// p - 1's attention, with ONE barrier per period (round 5):
-//   - V^T is double-buffered: head p's V goes to buffer p & 1 as soon as the
-//     producers' main loop ends, while the consumers read buffer (p - 1) & 1;
-//   - Q and K have one buffer: the consumers read them only in their score
-//     pass, then count themselves on an LDS word (qk_free); the producers
-//     write head p's Q / K once all four consumers of period p have counted
-//     (a bounded spin), so the split overlaps the consumers' softmax and P.V
-//     instead of sitting between two barriers.
-// Q / K rows are 64 B with their four 16-B segments XOR-swizzled by row
-// (conflict-free ds_read_b128 without padding).  The exp table holds only
-// magnitudes [lo_run, neg_n] (smaller ones are all 1.0; the lookup clamps with
-// one med3).  LDS: panel 57 KB + Q / K 32 KB + 2 x V^T 16.5 KB + exp 32.5 KB.
+// p - 1's attention; two barriers per period (the consumers are done with the
+// tiles; the tiles hold the next head).  LDS: the panel (58 KB), one head's
+// tiles (57 KB), the exp table (40 KB).
 constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
+#ifndef QKPC_CPRIO
+#define QKPC_CPRIO 0  // A/B: static issue priority of the consumer waves (round 4: 0, 1 and 2 within noise)
+#endif
 #ifndef QKPC_AHEAD
 #define QKPC_AHEAD 2  // the producers' weight blocks in flight (i8_core.h I8ResRing)
 #endif
-#ifndef QKPC_CPRIO
-#define QKPC_CPRIO 0  // A/B: static issue priority of the consumer waves (s_setprio)
-#endif
-#ifndef QKPC_SPIN_MAX
-#define QKPC_SPIN_MAX (1 << 20)  // bound of the producers' wait (never reached when the consumers run)
-#endif
-
-// halves offset of (row, 8-dim segment seg) in a swizzled 32-dim Q / K plane
-__device__ __forceinline__ int qk_sw(int row, int seg) { return row * 32 + ((seg ^ ((row >> 2) & 3)) << 3); }
 
 template <bool PK>
 __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
     constexpr int WT = W_Q4_0, D = 32, NP = QKPC_NP, NW = QKPC_NW, BM = 128, NT = NW * 64;
-    constexpr int NK = 128, VST = NK + 4, E = 384, NKB = E / 32;
+    constexpr int NK = 128, KST = D + 8, VST = NK + 4, E = 384, NKB = E / 32;
     using C = I8Chunk<BM, false>;
-    constexpr int QKB = 4 * NK * D * 2, VB = 2 * D * VST * 2;  // Qh Ql Kh Kl | Vh Vl of one buffer, bytes
+    constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
     __shared__ __attribute__((aligned(16))) char apanel[(E / I8_KC) * C::BYTES];
-    __shared__ __attribute__((aligned(16))) char tiles[QKB + 2 * VB];
-    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_PC_LDS];
+    __shared__ __attribute__((aligned(16))) char tiles[SLOT];
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     __shared__ int qtab[PK ? 4 : 1][4];     // query block -> {first tile row of its sentence, length, first query, vs}
     __shared__ uint8_t vslot[PK ? NK : 1];  // tile row -> V^T key slot
-    __shared__ int qk_free;                 // consumer waves done with the Q / K planes, all periods so far
     const int s0 = PK ? a.tiles[2 * blockIdx.x] : (int)blockIdx.x;
     const int ns = PK ? a.tiles[2 * blockIdx.x + 1] : 1;
     const int beg = a.offsets[s0], n = a.offsets[s0 + ns] - beg;
     if (n > NK || n <= 0 || ns > 4 || g.K != E || a.E != E) return;
-    if (a.expt.neg_n - a.expt.lo_run + 1 > EXP_PC_LDS || a.expt.lo_run < 0) return;  // (the host checks it too)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the role branches are scalar
     const int r = lane & 31, hh = lane >> 5;
-    // exp table: magnitudes lo .. neg_n (the last entry: the constant beyond neg_n)
-    const int elo = a.expt.lo_run, ehi = a.expt.neg_n;
-    {
-        const uint16_t *src = a.expt.compact + a.expt.pos_n + elo;
-        for (int i = tid; i <= ehi - elo; i += NT) etab[i] = src[i];
-    }
+    const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
+    for (int i = tid; i < a.expt.n_pad / 8; i += NT) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
     // the sentence's A panel: rows beg .. beg + 127 (rows past the batch are the
     // workspace's zero spare rows), chunk c = blocks 4c .. 4c + 3 in I8Chunk layout
     for (int it = tid; it < BM * NKB; it += NT) {
@@ -1621,8 +1600,7 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         ((uint16_t *)(buf + C::QB))[bb * BM + row] = ((const uint16_t *)g.A.d)[(int64_t)(beg + row) * NKB + b];
     }
     // the attention tiles start zero: rows / key slots no token writes stay zero for every head
-    for (int i = tid; i < (QKB + 2 * VB) / 16; i += NT) ((uint4 *)tiles)[i] = uint4{0u, 0u, 0u, 0u};
-    if (tid == 0) qk_free = 0;
+    for (int i = tid; i < SLOT / 16; i += NT) ((uint4 *)tiles)[i] = uint4{0u, 0u, 0u, 0u};
     if (PK && tid < NK) {
         int b = 0, vs = 0, qb_b = 0, qb_len = 0, qb_q = 0, qb_vs = 0, slt = 0;
         for (int j = 0; j < ns; j++) {
@@ -1646,8 +1624,8 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         }
     }
     __syncthreads();
-    auto plane = [&](int pl) -> _Float16 * {  // 0 Qh 1 Ql 2 Kh 3 Kl, 4 + 2 v Vh 5 + 2 v Vl of V buffer v
-        return (_Float16 *)(pl < 4 ? tiles + pl * NK * D * 2 : tiles + QKB + (pl - 4) * D * VST * 2);
+    auto plane = [&](int pl) -> _Float16 * {  // 0 Qh 1 Ql 2 Kh 3 Kl 4 Vh 5 Vl
+        return (_Float16 *)(pl < 4 ? tiles + pl * NK * KST * 2 : tiles + 4 * NK * KST * 2 + (pl - 4) * D * VST * 2);
     };
     const int H = a.H;
     if (wv < NP) {
@@ -1655,7 +1633,7 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
         // 64 (w & 1) .. + 63 as two 32-token t-tiles; lane (r, hh) holds token
         // 32 t + r of its t-tile t, head dims 16 hh .. 16 hh + 15 (i8_core.h)
         const int part = wv >> 1, tt0 = 2 * (wv & 1);
-        I8ResRing<WT, 1, QKPC_AHEAD> ring;  // head p + 1's first weight blocks load during head p's split and barrier
+        I8ResRing<WT, 1, QKPC_AHEAD> ring;  // head p + 1's first weight blocks load during head p's split and barriers
         ring.start(g, part);
         for (int p = 0; p <= H; p++) {
             float16v acc[1][2];
@@ -1671,18 +1649,10 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                     for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
                 }
                 i8_resident_mainloop<WT, BM, 1, 2>(g, apanel, 3 * p + part, tt0, acc, ring, p + 1 < H ? 3 * (p + 1) + part : -1);
-                STAMP(p, 1, NW);
-                if (part < 2) {
-                    // Q | K of head p replace head p - 1's, which the consumers of this
-                    // period read in their score pass: wait until all four have counted
-                    int spins = 0;
-                    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&qk_free, __ATOMIC_RELAXED,
-                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) <
-                               4 * (p + 1) &&
-                           ++spins < QKPC_SPIN_MAX)
-                        __builtin_amdgcn_s_sleep(1);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
+            }
+            STAMP(p, 1, NW);
+            __syncthreads();  // X: the consumers are done with head p - 1's tiles
+            if (p < H) {
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
                     const int row = 32 * (tt0 + t) + r;  // tile row (token of the tile)
@@ -1695,16 +1665,15 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                             hv[i >> 3][i & 7] = yh;
                             lv[i >> 3][i & 7] = (_Float16)(y - (float)yh);
                         }
-                        if (part < 2) {  // Q | K: row-major [token][dim], segments swizzled
-                            _Float16 *ph = plane(2 * part), *pl = plane(2 * part + 1);
-                            *(half8 *)(ph + qk_sw(row, 2 * hh)) = hv[0];
-                            *(half8 *)(ph + qk_sw(row, 2 * hh + 1)) = hv[1];
-                            *(half8 *)(pl + qk_sw(row, 2 * hh)) = lv[0];
-                            *(half8 *)(pl + qk_sw(row, 2 * hh + 1)) = lv[1];
-                        } else {  // V^T [dim][key slot] into buffer p & 1
+                        if (part < 2) {  // Q | K: row-major [token][dim]
+                            _Float16 *ph = plane(2 * part) + row * KST + 16 * hh, *pl = plane(2 * part + 1) + row * KST + 16 * hh;
+                            *(half8 *)ph = hv[0];
+                            *(half8 *)(ph + 8) = hv[1];
+                            *(half8 *)pl = lv[0];
+                            *(half8 *)(pl + 8) = lv[1];
+                        } else {  // V^T [dim][key slot]
                             const int slot = PK ? (int)vslot[row] : row;
-                            _Float16 *ph = plane(4 + 2 * (p & 1)) + (16 * hh) * VST + slot;
-                            _Float16 *pl = plane(5 + 2 * (p & 1)) + (16 * hh) * VST + slot;
+                            _Float16 *ph = plane(4) + (16 * hh) * VST + slot, *pl = plane(5) + (16 * hh) * VST + slot;
 #pragma unroll
                             for (int i = 0; i < 16; i++) {
                                 ph[i * VST] = hv[i >> 3][i & 7];
@@ -1715,16 +1684,15 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                 }
             }
             STAMP(p, 2, NW);
-            __syncthreads();  // head p's tiles are complete; the consumers are done with V buffer (p - 1) & 1
+            __syncthreads();  // Y: head p's tiles are complete
             STAMP(p + 1, 0, NW);
         }
     } else {
         // ---- consumer: query block qb of head p - 1 (32 queries of one sentence)
-        if (QKPC_CPRIO) __builtin_amdgcn_s_setprio(QKPC_CPRIO);
         const int qb = wv - NP;
         int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
         asm volatile("" : "+v"(lim));
-        const _Float16 *Qh = plane(0), *Ql = plane(1), *Kh = plane(2), *Kl = plane(3);
+        const _Float16 *Qh = plane(0), *Ql = plane(1), *Kh = plane(2), *Kl = plane(3), *Vh = plane(4), *Vl = plane(5);
         int kb = 0, len = n, qrel = 32 * qb, vs = 0;
         if constexpr (PK) {
             kb = qtab[qb][0];
@@ -1744,18 +1712,12 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
             asm volatile("" : "+v"(orow));
             attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), beg + orow, qrel + r < len, h, hh, 0);
         };
-        // this wave is done with the Q / K planes of this period (counted once per period)
-        auto release_qk = [&]() {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // its Q / K reads have completed
-            if (lane == 0) __hip_atomic_fetch_add(&qk_free, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        };
         for (int p = 0; p <= H; p++) {
             const int head = p - 1;
             const bool act = head >= 0 && qact;
             sum = 0;
             if (act) {
                 const int nkt = (len + 31) >> 5;
-                const _Float16 *Vh = plane(4 + 2 * (head & 1)), *Vl = plane(5 + 2 * (head & 1));
                 // key 32 kt + (j & 3) + 8 (j >> 2) + 4 hh valid while < len.  Opaque per
                 // head: loop-invariant, the 64 mask compares were hoisted out of the head
                 // loop as 64-bit lane masks and spilled the SGPRs
@@ -1764,21 +1726,11 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                 half8 qh[D / 16], ql[D / 16];
 #pragma unroll
                 for (int ks = 0; ks < D / 16; ks++) {
-                    qh[ks] = *(const half8 *)(Qh + qk_sw(qrow, 2 * ks + hh));
-                    ql[ks] = *(const half8 *)(Ql + qk_sw(qrow, 2 * ks + hh));
+                    qh[ks] = *(const half8 *)(Qh + qrow * KST + 16 * ks + 8 * hh);
+                    ql[ks] = *(const half8 *)(Ql + qrow * KST + 16 * ks + 8 * hh);
                 }
-                // S^T = K.Q^T for the 32-key tile at kt (three MFMAs per k-step, f32-level)
                 auto scores = [&](int kt) {
-                    float16v S = {};
-                    const int krow = kb + 32 * kt + r;
-#pragma unroll
-                    for (int ks = 0; ks < D / 16; ks++) {
-                        const int off = qk_sw(krow, 2 * ks + hh);
-                        const half8 kh = *(const half8 *)&Kh[off], kl = *(const half8 *)&Kl[off];
-                        S = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], S, 0, 0, 0);
-                        S = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], S, 0, 0, 0);
-                        S = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], S, 0, 0, 0);
-                    }
+                    float16v S = attn_qk<D>(Kh, Kl, KST, kb + 32 * kt, r, hh, qh, ql);
                     if (32 * kt + 32 > len) {
 #pragma unroll
                         for (int j = 0; j < 16; j++)
@@ -1801,17 +1753,11 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                         for (int j = 0; j < 16; j++) mx = fmaxf(mx, Sk[kt][j]);
                     }
                 }
-                release_qk();
                 mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
                 const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
                 // pass 2: p = exp_tab[fp16(s - max)], the exact integer sum of p * 2^24, and
                 // V.P over the key tiles in order
                 o[0] = float16v{};
-                // the table indexed from magnitude lo_run: one v_med3_u32 clamps the index
-                // to [lo_run, neg_n] and the base is biased by -lo_run once
-                const _Float16 *etb = (const _Float16 *)etab - elo;
-                uint32_t vlo = elo, vhi = ehi;
-                asm volatile("" : "+v"(vlo), "+v"(vhi));  // in VGPRs (one SGPR per VOP3 on gfx9)
 #pragma unroll
                 for (int kt = 0; kt < 4; kt++) {
                     if (kt >= nkt) continue;
@@ -1819,28 +1765,24 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
 #pragma unroll
                     for (int j = 0; j < 16; j += 2) {
                         const float2v d2 = mx2 - float2v{Sk[kt][j], Sk[kt][j + 1]} * sc2;
-                        half2v pv;
+                        uint16_t pb[2];
 #pragma unroll
                         for (int e = 0; e < 2; e++) {
-                            const uint32_t hm = f2h(d2[e]);  // |s - max| as fp16; masked: +inf -> the 0 entry
-                            uint32_t idx;
-                            asm("v_med3_u32 %0, %1, %2, %3" : "=v"(idx) : "v"(hm), "v"(vlo), "v"(vhi));
-                            pv[e] = etb[idx];
+                            const uint32_t hm = f2h(d2[e]);
+                            pb[e] = etab[epos + min(hm, (uint32_t)eneg)];
+                            ph[(j + e) >> 3][(j + e) & 7] = __builtin_bit_cast(_Float16, pb[e]);
                         }
-                        ph[j >> 3][j & 7] = pv[0];
-                        ph[j >> 3][(j & 7) + 1] = pv[1];
-                        const float2v pp = float2v{(float)pv[0], (float)pv[1]} * float2v{16777216.0f, 16777216.0f};
+                        const float2v pp = float2v{h2f(pb[0]), h2f(pb[1])} * float2v{16777216.0f, 16777216.0f};
                         sum += (uint32_t)pp[0] + (uint32_t)pp[1];
                     }
                     attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph, 0);
                 }
-            } else {
-                release_qk();
             }
             STAMP(p, 1, NW);
+            __syncthreads();  // X: this head's tiles may be overwritten
             if (act) store_ctx(head);
             STAMP(p, 2, NW);
-            __syncthreads();  // head p's tiles are complete (the producers' side of this barrier)
+            __syncthreads();  // Y
             STAMP(p + 1, 0, NW);
         }
     }
@@ -1896,6 +1838,22 @@ static int n_cus() {
 // rounds of n_cus tiles; the packed variant costs ~8 % more per workgroup
 // (measured: 414 vs 382 us at 1024 single-sentence tiles), so packing is used
 // only when it saves more than that in rounds.
+#ifdef PHASE_STAMPS
+// development builds only (tools/variant_lib.sh with -DPHASE_STAMPS=1): point
+// this translation unit's stamp buffer at a device buffer (tools/pipe_stamps.py)
+hipError_t stamps_set(unsigned long long *buf, int nblk) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &buf, sizeof(buf));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_nblk), &nblk, sizeof(nblk));
+    return e;
+}
+}  // namespace bertamd
+// (not declared in bert_amd.h: exists only in -DPHASE_STAMPS variant libraries)
+extern "C" __attribute__((visibility("default"))) int bert_amd_dev_stamps(void *buf, int nblk) {
+    return bertamd::stamps_set((unsigned long long *)buf, nblk) == hipSuccess ? 0 : -1;
+}
+namespace bertamd {
+#endif
+
 bool qkv_attention_pack_pays(int n_seqs, int n_tiles) {
     const int64_t c = n_cus(), plain = (n_seqs + c - 1) / c, packed = (n_tiles + c - 1) / c;
     return n_tiles < n_seqs && packed * 11 < plain * 10;

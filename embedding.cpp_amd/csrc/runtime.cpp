@@ -77,7 +77,6 @@ void set_err(const char *fmt, ...) {
 struct CompactTable {
     std::vector<uint16_t> compact;
     int pos_n = 0, neg_n = 0, pos_identity = 0;
-    int lo_run = 0;  // magnitudes 0 .. lo_run of the negative side share the value of magnitude 0
     uint32_t neg_const = 0;
 };
 CompactTable compact_table(const std::vector<uint16_t> &full, bool identity_tail, int pos_n_fixed) {
@@ -99,7 +98,6 @@ CompactTable compact_table(const std::vector<uint16_t> &full, bool identity_tail
     c.compact[(size_t)(c.pos_n + c.neg_n)] = (uint16_t)c.neg_const;
     for (int h = 0; h < c.pos_n; h++) c.compact[(size_t)h] = full[(size_t)h];
     for (int m = 0; m < c.neg_n; m++) c.compact[(size_t)(c.pos_n + m)] = full[(size_t)(0x8000 | m)];
-    while (c.lo_run + 1 < c.neg_n && full[(size_t)(0x8000 | (c.lo_run + 1))] == full[0x8000]) c.lo_run++;
     // self-check of the device lookup rules on every finite pattern they serve
     // (kernels.hip gelu_lookup; soft_max's exp lookup only sees s - max <= 0)
     for (uint32_t h = 0; h < 65536; h++) {
@@ -160,7 +158,6 @@ HalfTable half_table(const uint16_t *full, const uint16_t *compact, const Compac
     t.full = full;
     t.compact = compact;
     t.pos_n = c.pos_n;
-    t.lo_run = c.lo_run;
     t.neg_n = c.neg_n;
     t.n_pad = (int)c.compact.size();
     t.pos_identity = c.pos_identity;
@@ -1399,8 +1396,7 @@ bert_ctx *load_impl(const char *fname, const int32_t *devices, int32_t n_devices
         set_err("fp16 GELU/exp table self-check failed: the device lookup rules do not reproduce this host's tables");
         return nullptr;
     }
-    if ((int)tables().gelu_pair.size() > HALF_TABLE_LDS || (int)tables().exp_c.compact.size() > EXP_TABLE_LDS ||
-        tables().exp_c.neg_n - tables().exp_c.lo_run + 1 > EXP_PC_LDS) {
+    if ((int)tables().gelu_pair.size() > HALF_TABLE_LDS || (int)tables().exp_c.compact.size() > EXP_TABLE_LDS) {
         set_err("this host's libm gives fp16 GELU/exp tables whose compact part exceeds LDS (%zu, %zu entries)",
                 tables().gelu_pair.size(), tables().exp_c.compact.size());
         return nullptr;

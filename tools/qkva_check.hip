@@ -87,11 +87,6 @@ int main() {
     a.expt.compact = up(comp);
     a.expt.pos_n = 1;
     a.expt.neg_n = neg_n;
-    {  // magnitudes 0 .. lo_run give 1.0 (kernels.h HalfTable::lo_run; the producer / consumer kernel clamps to it)
-        int lo = 0;
-        while (lo + 1 < neg_n && full[0x8000 | (lo + 1)] == full[0x8000]) lo++;
-        a.expt.lo_run = lo;
-    }
     a.expt.n_pad = (int)comp.size();
     std::vector<std::vector<uint16_t>> out(2);
     for (int G = 1; G <= 2; G++) {

@@ -125,11 +125,6 @@ int main(int argc, char **argv) {
     a.expt.compact = d_comp;
     a.expt.pos_n = 1;
     a.expt.neg_n = neg_n;
-    {  // magnitudes 0 .. lo_run give 1.0 (kernels.h HalfTable::lo_run; the producer / consumer kernel clamps to it)
-        int lo = 0;
-        while (lo + 1 < neg_n && full[0x8000 | (lo + 1)] == full[0x8000]) lo++;
-        a.expt.lo_run = lo;
-    }
     a.expt.n_pad = (int)comp.size();
     void *cq, *cd;
     CK(hipMalloc(&cq, (size_t)Mpad * E));
