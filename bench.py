@@ -561,7 +561,8 @@ def main():
                                         us_p10=round(float(np.percentile(ts, 10)) * 1e6, 1),
                                         us_p90=round(float(np.percentile(ts, 90)) * 1e6, 1),
                                         launches_per_call=int(sum(c for _, c in lp.values())),
-                                        device_us=round(sum(ms for ms, _ in lp.values()) * 1e3, 1))
+                                        device_us=round(sum(ms for ms, _ in lp.values()) * 1e3, 1),
+                                        kernel_us={k: round(ms * 1e3 / max(c, 1), 1) for k, (ms, c) in lp.items()})
         latency["note"] = ("bert_eval, one sentence, host buffers (ids H2D + embedding D2H + stream sync), "
                            f"median of {args.latency_runs}; device_us = sum of the call's kernel durations "
                            "(HIP events, separate profiled call)")

@@ -15,8 +15,18 @@ namespace bertamd {
 #ifndef I8_Q41_GENERIC
 #define I8_Q41_GENERIC 0
 #endif
+// Q4_1 scale products on the bf16 MFMA: d_w * d_a and m_w * s_a (fp16 x f32)
+// as sums of exact bf16 x bf16 partial products (d_w = w0 + w1, d_a = a0 + a1
+// + a2 in bf16 parts) in one v_mfma_f32_32x32x16_bf16 (32 cycles) instead of
+// the f32 MFMA (64 cycles per 32 x 32 tile); the d_a / s_a parts are made once
+// per chunk when the A chunk is staged (I8Chunk holds them as packed 16-byte
+// MFMA operands).  tools/mfma_bf16_split_probe.hip checks the rounding.
+#ifndef I8_Q41_BF16
+#define I8_Q41_BF16 0
+#endif
 
 typedef int int4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef int int16v __attribute__((ext_vector_type(16)));
 
 
@@ -27,11 +37,32 @@ constexpr int I8_LDQ = I8_KC + 16;  // token row stride of the LDS chunk, bytes:
 
 template <int BM, bool Q1>
 struct I8Chunk {
+    static constexpr bool BFS = Q1 && I8_Q41_BF16;  // Q8_1 scales as packed bf16-part operands
     static constexpr int QB = BM * I8_LDQ;          // int8 q [BM][LDQ]
-    static constexpr int DB = 4 * BM * (Q1 ? 4 : 2);  // d_a [4][BM]: fp16 (Q8_0) | f32 (Q8_1)
-    static constexpr int SB = Q1 ? 4 * BM * 4 : 0;  // f32 s_a [4][BM] (Q8_1: s = d * sum q, ggml quantize_row_q8_1)
+    // d_a [4][BM]: fp16 (Q8_0) | f32 (Q8_1) | 16-byte bf16-part operand (BFS)
+    static constexpr int DB = 4 * BM * (BFS ? 16 : Q1 ? 4 : 2);
+    // s_a [4][BM] (Q8_1: s = d * sum q, ggml quantize_row_q8_1): f32 | 16-byte operand (BFS)
+    static constexpr int SB = Q1 ? 4 * BM * (BFS ? 16 : 4) : 0;
     static constexpr int BYTES = QB + DB + SB;
 };
+
+// x = p0 + p1 + p2 exactly as bf16 values (x has <= 24 significant bits), as
+// the packed MFMA operand {p0, p1, p2, p0, p1, p2, 0, 0}; the weight side is
+// {w0, w0, w0, w1, w1, w1, 0, 0} (i8_wparts), so k = 0..5 hold the six cross
+// products of the two splits
+__device__ __forceinline__ int4v i8_aparts(float x) {
+    const uint32_t b = __float_as_uint(x), h0 = b >> 16;
+    const float r = x - __uint_as_float(b & 0xffff0000u);  // exact
+    const uint32_t br = __float_as_uint(r), h1 = br >> 16;
+    const uint32_t h2 = __float_as_uint(r - __uint_as_float(br & 0xffff0000u)) >> 16;  // exact, <= 8 bits
+    return int4v{(int)(h0 | (h1 << 16)), (int)(h2 | (h0 << 16)), (int)(h1 | (h2 << 16)), 0};
+}
+// an fp16-valued weight scale (<= 11 significant bits) as {w0, w0, w0, w1, w1, w1, 0, 0}
+__device__ __forceinline__ int4v i8_wparts(float w) {
+    const uint32_t b = __float_as_uint(w), h0 = b >> 16;
+    const uint32_t h1 = __float_as_uint(w - __uint_as_float(b & 0xffff0000u)) >> 16;  // exact
+    return int4v{(int)(h0 | (h0 << 16)), (int)(h0 | (h1 << 16)), (int)(h1 | (h1 << 16)), 0};
+}
 
 // The (token, block) items of an A chunk in flight: 32 q bytes + d each
 // (separate arrays: an array of structs carried across the chunk loop was
@@ -82,7 +113,7 @@ __device__ __forceinline__ void i8_stage_store(const I8Items<(4 * BM + NT - 1) /
             q[1] = st.q1[it];
             if constexpr (WT == W_Q4_0)
                 ((uint16_t *)(buf + C::QB))[bb * BM + r] = st.d16[it];
-            else
+            else if constexpr (!C::BFS)
                 ((float *)(buf + C::QB))[bb * BM + r] = st.d[it];
             if constexpr (WT == W_Q4_1) {
                 // ggml quantize_row_q8_1: s = d * (float) sum_j q_j (int sum, f32 product)
@@ -92,7 +123,13 @@ __device__ __forceinline__ void i8_stage_store(const I8Items<(4 * BM + NT - 1) /
                 for (int j = 0; j < 4; j++) s = __builtin_amdgcn_sdot4(a[j], 0x01010101, s, false);
 #pragma unroll
                 for (int j = 0; j < 4; j++) s = __builtin_amdgcn_sdot4(b[j], 0x01010101, s, false);
-                ((float *)(buf + C::QB + C::DB))[bb * BM + r] = st.d[it] * (float)s;
+                const float sv = st.d[it] * (float)s;
+                if constexpr (C::BFS) {
+                    ((int4v *)(buf + C::QB))[bb * BM + r] = i8_aparts(st.d[it]);
+                    ((int4v *)(buf + C::QB + C::DB))[bb * BM + r] = i8_aparts(sv);
+                } else {
+                    ((float *)(buf + C::QB + C::DB))[bb * BM + r] = sv;
+                }
             }
         }
     }
@@ -116,6 +153,9 @@ struct I8AOps {
     int4v xa[T];
     uint32_t d16[T];  // Q4_0: fp16 d_a (the one-hot operand is built where it is used)
     float da[T];      // Q4_1
+#if I8_Q41_BF16
+    int4v dp[T];      // Q4_1 with I8_Q41_BF16: d_a as its bf16-part operand
+#endif
 };
 
 template <int WT, int BM, int T, int BB>
@@ -128,6 +168,10 @@ __device__ __forceinline__ void i8_aops(I8AOps<T> &o, const char *buf, int tt0) 
         o.xa[t] = *(const int4v *)(buf + r * I8_LDQ + 32 * BB + 16 * hh);
         if constexpr (WT == W_Q4_0) {
             o.d16[t] = ((const uint16_t *)(buf + C::QB))[BB * BM + r];
+        } else if constexpr (C::BFS) {
+#if I8_Q41_BF16
+            o.dp[t] = ((const int4v *)(buf + C::QB))[BB * BM + r];
+#endif
         } else {
             o.da[t] = ((const float *)(buf + C::QB))[BB * BM + r];
         }
@@ -215,14 +259,31 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
     }
 #else
     if constexpr (WT == W_Q4_1 && (BB & 1)) {
-        // m_w * s_a of blocks b - 1 (k = 0, lanes 0-31) and b (k = 1, lanes 32-63)
-        const float *sbuf = (const float *)(buf + C::QB + C::DB);
+        if constexpr (C::BFS) {
+            // m_w * s_a of blocks b - 1 (k = 0..5, lanes 0-31) and b (k = 8..13, lanes
+            // 32-63) as bf16 partial products, one bf16 MFMA
+            const int4v *sbuf = (const int4v *)(buf + C::QB + C::DB);
+            int4v mp[F];
 #pragma unroll
-        for (int t = 0; t < T; t++) {
-            const float sa = sbuf[(BB - 1 + hh) * BM + 32 * (tt0 + t) + l32];
+            for (int f = 0; f < F; f++) mp[f] = i8_wparts(hh ? wm[f][BB] : wm[f][BB - 1]);
 #pragma unroll
-            for (int f = 0; f < F; f++)
-                acc[f][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh ? wm[f][BB] : wm[f][BB - 1], sa, acc[f][t], 0, 0, 0);
+            for (int t = 0; t < T; t++) {
+                const int4v sp = sbuf[(BB - 1 + hh) * BM + 32 * (tt0 + t) + l32];
+#pragma unroll
+                for (int f = 0; f < F; f++)
+                    acc[f][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, mp[f]),
+                                                                        __builtin_bit_cast(bf16x8, sp), acc[f][t], 0, 0, 0);
+            }
+        } else {
+            // m_w * s_a of blocks b - 1 (k = 0, lanes 0-31) and b (k = 1, lanes 32-63)
+            const float *sbuf = (const float *)(buf + C::QB + C::DB);
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                const float sa = sbuf[(BB - 1 + hh) * BM + 32 * (tt0 + t) + l32];
+#pragma unroll
+                for (int f = 0; f < F; f++)
+                    acc[f][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh ? wm[f][BB] : wm[f][BB - 1], sa, acc[f][t], 0, 0, 0);
+            }
         }
     }
 #endif
@@ -238,12 +299,27 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
             oh[t][BB >> 1] = (int)v;
         }
     }
+#if I8_Q41_BF16
+    int4v wp[F];  // Q4_1: d_w of block BB as its bf16-part operand (zero in lanes 32-63, as wd)
+    if constexpr (C::BFS) {
+#pragma unroll
+        for (int f = 0; f < F; f++) wp[f] = i8_wparts(wd[f][BB]);
+    }
+#endif
     auto ddmfma = [&](int f, int t) {
-        if constexpr (WT == W_Q4_0)
+        if constexpr (WT == W_Q4_0) {
             return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ws[f]),
                                                           __builtin_bit_cast(half8, oh[t]), zf, 0, 0, 0);
-        else
+        } else if constexpr (C::BFS) {
+#if I8_Q41_BF16
+            return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wp[f]),
+                                                           __builtin_bit_cast(bf16x8, cur.dp[t]), zf, 0, 0, 0);
+#else
+            return zf;
+#endif
+        } else {
             return __builtin_amdgcn_mfma_f32_32x32x2f32(wd[f][BB], cur.da[t], zf, 0, 0, 0);
+        }
     };
     // software pipeline over the F x T tiles: tile p + 1's two MFMAs are in
     // flight while tile p is folded

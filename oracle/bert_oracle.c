@@ -630,6 +630,31 @@ int oracle_embed_ln(void *vm, const int32_t *tokens, int N, float *x_out) {
     return 0;
 }
 
+/* Attention arithmetic (NOT a ggml build: a diagnostic).
+     0: ggml's — K.Q and V.P as f32 dot products (in the dot variant's order),
+        P scaled by 1/sum before V.P;
+     1: the GPU kernels' operand form — K, Q and V carried as fp16 hi + lo
+        pairs (hi = fp16(x), lo = fp16(x - hi): 22 significant bits instead of
+        24), K.Q = sum(kh qh + kh ql + kl qh) (the lo.lo term dropped), V.P on
+        the table's fp16 p with the 1/sum scale applied after; each dot summed
+        exactly and rounded once (the MFMA's own f32 accumulation order is not
+        restated).  Lets the tests measure how much of the GPU's distance to
+        ggml comes from the attention operands rather than the GEMMs. */
+static int g_attn_form = 0;
+void oracle_set_attn_form(int f) { g_attn_form = f; }
+static float split22(float x) {
+    const float hi = F16(H16(x));
+    return (float)((double)hi + (double)F16(H16(x - hi)));
+}
+static float dot_split(int n, const float *k, const float *q) {
+    double s = 0.0;
+    for (int i = 0; i < n; i++) {
+        const double kh = F16(H16(k[i])), kl = (double)k[i] - kh, qh = F16(H16(q[i])), ql = (double)q[i] - qh;
+        s += kh * qh + kh * ql + kl * qh;
+    }
+    return (float)s;
+}
+
 /* one encoder layer il on x[N][E] in place (bert.cpp:900-993) */
 static void encoder_layer(const omodel *m, int il, float *x, int N) {
     const int E = m->n_embd, I = m->n_inter, H = m->n_head, D = E / H;
@@ -656,10 +681,14 @@ static void encoder_layer(const omodel *m, int il, float *x, int N) {
                 qh[t * D + j] = Q[(size_t)t * E + h * D + j];
                 vt[(size_t)j * N + t] = V[(size_t)t * E + h * D + j]; /* ggml_cont(transpose(V)) */
             }
+        if (g_attn_form == 1) { /* the GPU kernels' operand form (see oracle_set_attn_form) */
+            for (int i = 0; i < N * D; i++) { kh[i] = split22(kh[i]); qh[i] = split22(qh[i]); vt[i] = split22(vt[i]); }
+        }
         for (int q = 0; q < N; q++) {
             float mx = -INFINITY;
             for (int k = 0; k < N; k++) {
-                P[k] = dot_f32(D, kh + k * D, qh + q * D) * kq_scale;  /* mul_mat(K,Q), scale */
+                const float s = g_attn_form == 1 ? dot_split(D, kh + k * D, qh + q * D) : dot_f32(D, kh + k * D, qh + q * D);
+                P[k] = s * kq_scale;  /* mul_mat(K,Q), scale */
                 mx = P[k] > mx ? P[k] : mx;
             }
             double sum = 0.0;
@@ -670,6 +699,14 @@ static void encoder_layer(const omodel *m, int il, float *x, int N) {
                 P[k] = val;
             }
             const float r = (float)(1.0 / sum);
+            if (g_attn_form == 1) { /* V.P on the table's fp16 values, then the 1/sum scale */
+                for (int j = 0; j < D; j++) {
+                    double acc = 0.0;
+                    for (int k = 0; k < N; k++) acc += (double)P[k] * (double)vt[(size_t)j * N + k];
+                    ctx[(size_t)q * E + h * D + j] = (float)acc * r;
+                }
+                continue;
+            }
             for (int k = 0; k < N; k++) P[k] *= r;
             for (int j = 0; j < D; j++) ctx[(size_t)q * E + h * D + j] = dot_f32(N, vt + (size_t)j * N, P);
         }

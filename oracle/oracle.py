@@ -54,6 +54,7 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_int8)]
         L.oracle_max_threads.restype = ctypes.c_int
         L.oracle_set_dot_variant.argtypes = [ctypes.c_int]
+        L.oracle_set_attn_form.argtypes = [ctypes.c_int]
         L.oracle_embed_ln.restype = ctypes.c_int
         L.oracle_embed_ln.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_float)]
@@ -70,6 +71,15 @@ def lib() -> ctypes.CDLL:
 # dot-kernel summation orders of the ggml builds the oracle can replay
 # (bert_oracle.c oracle_set_dot_variant): the checker uses "avx2"
 DOT_VARIANTS = {"avx2": 0, "generic": 1, "lanes16": 2}
+
+
+# attention arithmetic (bert_oracle.c oracle_set_attn_form): "ggml" (the
+# checker), or "gpu_operands" — a diagnostic, not a ggml build
+ATTN_FORMS = {"ggml": 0, "gpu_operands": 1}
+
+
+def set_attn_form(name: str) -> None:
+    lib().oracle_set_attn_form(ATTN_FORMS[name])
 
 
 def set_dot_variant(name: str) -> None:

@@ -137,6 +137,41 @@ def test_c5_vs_each_ggml_build_by_projection_form(opts, model_dir):
     assert min(t.values()) <= float(np.max(parity_bound(meta))), t
 
 
+@pytest.mark.skipif(os.environ.get("BERT_AMD_PARITY_DIAG") != "1", reason="diagnostic (BERT_AMD_PARITY_DIAG=1)")
+@pytest.mark.parametrize("opts", [None, {"i8": "all"}])
+@pytest.mark.parametrize("case", ["c5_bge_q4_1", "c3_minilm_q4_0", "minilm_q4_1"])
+def test_attention_operand_form_diagnostic(case, opts, model_dir):
+    """How much of the GPU's distance to ggml comes from the attention
+    operands: the GPU against the oracle with ggml's attention and with the
+    GPU kernels' operand form (fp16 hi/lo K, Q, V; oracle.set_attn_form
+    "gpu_operands", a diagnostic restatement, not a ggml build), under the
+    AVX2 and plain-C orders.  Recorded in gpurun_out/attnform_<case>_<opts>.json
+    (DESIGN.md §4)."""
+    import oracle
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    m = bertlib.BertModel(p, options=opts)
+    try:
+        got = m.eval_batch(toks)
+    finally:
+        m.close()
+    orc = oracle.Oracle(p)
+    res = {}
+    try:
+        for form in ("ggml", "gpu_operands"):
+            oracle.set_attn_form(form)
+            for var in ("avx2", "generic"):
+                oracle.set_dot_variant(var)
+                ref = orc.eval_batch(toks, 0)
+                res[f"{var}+{form}"] = float((1 - cos(got, ref)).max())
+    finally:
+        oracle.set_dot_variant("avx2")
+        oracle.set_attn_form("ggml")
+    tag = "default" if not opts else "i8all"
+    print(f"{case} [{tag}]: GPU vs oracle forms {res}")
+    _record(f"attnform_{case}_{tag}.json", res)
+
+
 @pytest.mark.xfail(strict=True, reason="ggml's own builds differ by 1-cos 1.8e-3 / 2.3e-3 on these inputs "
                                        "(fixture ggml_order_spread_1mcos): cos >= 0.9999 is out of reach "
                                        "for any implementation that is not the AVX2 build itself")

@@ -32,6 +32,7 @@ from make_golden import ensure_model, load_case, sha256
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIAG = os.environ.get("BERT_AMD_PARITY_DIAG") == "1"
 
 
 def cos_rows(a, b):
@@ -116,6 +117,17 @@ def test_layer_by_layer_parity(case, sents, opts, model_dir):
                     spreads.append((1 - cos_rows(alt, loc), max_ulp(alt, loc)))
                     # the GPU's own layer against that build's layer on the same input
                     row[f"local_{var}_1mcos"] = 1 - cos_rows(g, alt)
+                if DIAG:
+                    # diagnostic (BERT_AMD_PARITY_DIAG=1): the oracle with the GPU's attention
+                    # operand form (oracle.set_attn_form, not a ggml build) under each order
+                    oracle.set_attn_form("gpu_operands")
+                    try:
+                        for var in ("avx2", "generic"):
+                            oracle.set_dot_variant(var)
+                            row[f"local_{var}_gpuattn_1mcos"] = 1 - cos_rows(g, orc.layer(s - 1, x_in))
+                    finally:
+                        oracle.set_dot_variant("avx2")
+                        oracle.set_attn_form("ggml")
                 row["spread_1mcos"] = max(sp[0] for sp in spreads)
                 row["spread_ulp"] = max(sp[1] for sp in spreads)
             rows.append(row)
@@ -143,7 +155,7 @@ def test_layer_by_layer_parity(case, sents, opts, model_dir):
     loc = [r["local_1mcos"] for r in rows if r["stage"]]
     spr = [r["spread_1mcos"] for r in rows if r["stage"]]
     print(f"mean local 1-cos {np.mean(loc):.2e}, mean ggml spread {np.mean(spr):.2e}, max local {max(loc):.2e}")
-    for var in ("generic", "lanes16"):
+    for var in ("generic", "lanes16") + (("avx2_gpuattn", "generic_gpuattn") if DIAG else ()):
         lv = [r[f"local_{var}_1mcos"] for r in rows if r["stage"]]
         print(f"  mean local 1-cos vs the {var} build {np.mean(lv):.2e} (max {max(lv):.2e}, "
               f"layers where the GPU equals it bit for bit: {sum(v == 0.0 for v in lv)} of {len(lv)})")
