@@ -22,9 +22,9 @@ step bench 600 python3 "$B" --steps 20 --warmup 5 --cpu-sample 256
 # kernel stats and counters per whole-batch launch (one row group; bench.py's own
 # event pass does the same), so rocprofv3 averages match the bench's roofline
 export BERT_AMD_SPLIT=0
-step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o $TAG -- python3 "$B" --steps 10 --warmup 3 --cpu-sample 0 --ragged-steps 0 --host-runs 0 --consumer-texts 0
-step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0 --ragged-steps 0 --host-runs 0 --consumer-texts 0
-step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0 --ragged-steps 0 --host-runs 0 --consumer-texts 0
+step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o $TAG -- python3 "$B" --steps 10 --warmup 3 --cpu-sample 0 --ragged-steps 0 --host-runs 0 --consumer-texts 0 --latency-runs 0 --load-replicas 0
+step fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0 --ragged-steps 0 --host-runs 0 --consumer-texts 0 --latency-runs 0 --load-replicas 0
+step write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o $TAG -- python3 "$B" --steps 2 --warmup 1 --profile-steps 1 --cpu-sample 0 --ragged-steps 0 --host-runs 0 --consumer-texts 0 --latency-runs 0 --load-replicas 0
 F=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -1)
 W=$(find "$OUT/write" -name '*counter_collection.csv' | head -1)
 python3 tools/hbm_summary.py "$OUT/fetch" "$OUT/write" "$TAG bench (C3 minilm q4_0 1024x128)" > "$OUT/${TAG}_pmc_hbm.txt"
