@@ -15,7 +15,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wn
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
 HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
 
-all: $(BUILD)/libbert.so $(BUILD)/div_check $(BUILD)/qkva_check
+all: $(BUILD)/libbert.so $(BUILD)/div_check $(BUILD)/qkva_check $(BUILD)/mfma_bf16_split_probe
 
 $(BUILD)/obj/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/bert.h include/bert_amd.h
 	@mkdir -p $(dir $@)
@@ -49,6 +49,11 @@ $(BUILD)/gemm_bench: tools/gemm_bench.hip embedding.cpp_amd/csrc/kernels.hip emb
 $(BUILD)/div_check: tools/div_check.hip
 	@mkdir -p $(BUILD)
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -Wno-unused-value -Wno-unused-result $< -o $@
+
+# device probe of the bf16 partial-product scale products (tests/test_gpu_parity.py)
+$(BUILD)/mfma_bf16_split_probe: tools/mfma_bf16_split_probe.hip
+	@mkdir -p $(BUILD)
+	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@
 
 # development timing harness for the int8-MFMA GEMMs (not shipped)
 

@@ -52,7 +52,7 @@ template <int WT, int NWV, int F, int T>
 __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
     constexpr int NT = NWV * 64, BM = 32 * T, BN = 32 * NWV * F;
     constexpr bool PIPE = NWV <= 12;
-    using C = I8Chunk<BM, WT == W_Q4_1>;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ __attribute__((aligned(16))) uint16_t gtab[GELU_FLAT_LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
@@ -143,7 +143,7 @@ template <int WT, bool OV = I8_LN_OV>
 __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles) {
     constexpr int NT = 768, BM = 64, F = 1, T = 2, NCOL = 384, NWV = 12;
     constexpr int XCH = BM * NCOL / 4;  // 16-byte chunks of the residual tile
-    using C = I8Chunk<BM, WT == W_Q4_1>;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ double red[2][NWV][BM];
     __shared__ __attribute__((aligned(16))) float xs[BM * NCOL];
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
 template <int WT>
 __global__ __launch_bounds__(512) void i8_resid_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
     constexpr int NT = 512, BM = 64, BN = 256, F = 1, T = 2;
-    using C = I8Chunk<BM, WT == W_Q4_1>;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int nwg = n_mtiles * n_ntiles;
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(512) void i8_resid_kernel(GemmArgs g, int n_mtiles,
 template <int WT>
 __global__ __launch_bounds__(768) void i8_qkv_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
     constexpr int NT = 768, BM = 64, BN = 384, F = 1, T = 2;
-    using C = I8Chunk<BM, WT == W_Q4_1>;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int nwg = n_mtiles * n_ntiles, E = g.N / 3, D = g.head_dim;
@@ -465,6 +465,7 @@ hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipSt
     switch (wtype) {
         case W_Q4_0: return i8_gemm_t<W_Q4_0>(epi, a, Mpad, s);
         case W_Q4_1: return i8_gemm_t<W_Q4_1>(epi, a, Mpad, s);
+        case W_Q4_1B: return i8_gemm_t<W_Q4_1B>(epi, a, Mpad, s);
     }
     return hipErrorInvalidValue;
 }

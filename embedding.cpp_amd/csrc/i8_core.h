@@ -15,15 +15,13 @@ namespace bertamd {
 #ifndef I8_Q41_GENERIC
 #define I8_Q41_GENERIC 0
 #endif
-// Q4_1 scale products on the bf16 MFMA: d_w * d_a and m_w * s_a (fp16 x f32)
-// as sums of exact bf16 x bf16 partial products (d_w = w0 + w1, d_a = a0 + a1
-// + a2 in bf16 parts) in one v_mfma_f32_32x32x16_bf16 (32 cycles) instead of
-// the f32 MFMA (64 cycles per 32 x 32 tile); the d_a / s_a parts are made once
-// per chunk when the A chunk is staged (I8Chunk holds them as packed 16-byte
-// MFMA operands).  tools/mfma_bf16_split_probe.hip checks the rounding.
-#ifndef I8_Q41_BF16
-#define I8_Q41_BF16 0
-#endif
+// W_Q4_1B (kernels.h): Q4_1's scale products on the bf16 MFMA — d_w * d_a and
+// m_w * s_a (fp16 x f32) as sums of exact bf16 x bf16 partial products (d_w =
+// w0 + w1, d_a = a0 + a1 + a2 in bf16 parts) in one v_mfma_f32_32x32x16_bf16
+// (32 cycles) instead of the f32 MFMA (64 cycles per 32 x 32 tile); the d_a /
+// s_a parts are made once per chunk when the A chunk is staged (I8Chunk holds
+// them as packed 16-byte MFMA operands).  tools/mfma_bf16_split_probe.hip
+// checks the rounding on the device.
 
 typedef int int4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -35,9 +33,9 @@ typedef int int16v __attribute__((ext_vector_type(16)));
 constexpr int I8_KC = 128;          // K per LDS chunk: 4 quant blocks (one scale vector)
 constexpr int I8_LDQ = I8_KC + 16;  // token row stride of the LDS chunk, bytes: ds_read_b128 conflict-free
 
-template <int BM, bool Q1>
+template <int BM, bool Q1, bool BF = false>
 struct I8Chunk {
-    static constexpr bool BFS = Q1 && I8_Q41_BF16;  // Q8_1 scales as packed bf16-part operands
+    static constexpr bool BFS = Q1 && BF;  // Q8_1 scales as packed bf16-part operands (W_Q4_1B)
     static constexpr int QB = BM * I8_LDQ;          // int8 q [BM][LDQ]
     // d_a [4][BM]: fp16 (Q8_0) | f32 (Q8_1) | 16-byte bf16-part operand (BFS)
     static constexpr int DB = 4 * BM * (BFS ? 16 : Q1 ? 4 : 2);
@@ -101,7 +99,7 @@ __device__ __forceinline__ void i8_stage_load(I8Items<(4 * BM + NT - 1) / NT> &s
 template <int WT, int BM, int NT>
 __device__ __forceinline__ void i8_stage_store(const I8Items<(4 * BM + NT - 1) / NT> &st, char *buf) {
     constexpr int IT = (4 * BM + NT - 1) / NT;
-    using C = I8Chunk<BM, WT == W_Q4_1>;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
 #pragma unroll
     for (int it = 0; it < IT; it++) {
         int item = threadIdx.x + it * NT;
@@ -115,7 +113,7 @@ __device__ __forceinline__ void i8_stage_store(const I8Items<(4 * BM + NT - 1) /
                 ((uint16_t *)(buf + C::QB))[bb * BM + r] = st.d16[it];
             else if constexpr (!C::BFS)
                 ((float *)(buf + C::QB))[bb * BM + r] = st.d[it];
-            if constexpr (WT == W_Q4_1) {
+            if constexpr (wt_q41(WT)) {
                 // ggml quantize_row_q8_1: s = d * (float) sum_j q_j (int sum, f32 product)
                 const int4v a = st.q0[it], b = st.q1[it];
                 int s = 0;
@@ -153,14 +151,12 @@ struct I8AOps {
     int4v xa[T];
     uint32_t d16[T];  // Q4_0: fp16 d_a (the one-hot operand is built where it is used)
     float da[T];      // Q4_1
-#if I8_Q41_BF16
-    int4v dp[T];      // Q4_1 with I8_Q41_BF16: d_a as its bf16-part operand
-#endif
+    int4v dp[T];      // W_Q4_1B: d_a as its bf16-part operand
 };
 
 template <int WT, int BM, int T, int BB>
 __device__ __forceinline__ void i8_aops(I8AOps<T> &o, const char *buf, int tt0) {
-    using C = I8Chunk<BM, WT == W_Q4_1>;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
     const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
 #pragma unroll
     for (int t = 0; t < T; t++) {
@@ -169,9 +165,7 @@ __device__ __forceinline__ void i8_aops(I8AOps<T> &o, const char *buf, int tt0) 
         if constexpr (WT == W_Q4_0) {
             o.d16[t] = ((const uint16_t *)(buf + C::QB))[BB * BM + r];
         } else if constexpr (C::BFS) {
-#if I8_Q41_BF16
             o.dp[t] = ((const int4v *)(buf + C::QB))[BB * BM + r];
-#endif
         } else {
             o.da[t] = ((const float *)(buf + C::QB))[BB * BM + r];
         }
@@ -214,7 +208,7 @@ struct I8Pipe {
         i8_stage_load<WT, BM, NT>(st, g.A, g.K, m0, c * I8_KC);
 #pragma unroll
         for (int f = 0; f < F; f++) {
-            if constexpr (WT == W_Q4_1) {
+            if constexpr (wt_q41(WT)) {
                 wdr[f] = i8_wvec(g.Wi.d, nkb, ft0 + f, c);
                 wmr[f] = i8_wvec(g.Wi.m, nkb, ft0 + f, c);
             } else {
@@ -238,7 +232,7 @@ template <int WT, int BM, int F, int T, int BB, bool PIPE>
 __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (&wfc)[F], const int4v (&ws)[F],
                                          const float4v (&wd)[F], const float4v (&wm)[F], const I8AOps<T> &cur,
                                          I8AOps<T> &nxt, float16v (&acc)[F][T]) {
-    using C = I8Chunk<BM, WT == W_Q4_1>;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
     const int lane = threadIdx.x & 63, l32 = lane & 31, hh = lane >> 5;
     const float16v zf = {};
     if constexpr (BB < 3) i8_aops<WT, BM, T, BB + 1>(nxt, buf, tt0);
@@ -247,7 +241,7 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
     // (float) isum, m_w * s_a) — m_w * s_a rounded on its own (the f32 MFMA with
     // one nonzero product per output), then one fma and one add per output
     float16v ms[F][T];
-    if constexpr (WT == W_Q4_1) {
+    if constexpr (wt_q41(WT)) {
         const float *sbuf = (const float *)(buf + C::QB + C::DB);
 #pragma unroll
         for (int t = 0; t < T; t++) {
@@ -258,7 +252,7 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
         }
     }
 #else
-    if constexpr (WT == W_Q4_1 && (BB & 1)) {
+    if constexpr (wt_q41(WT) && (BB & 1)) {
         if constexpr (C::BFS) {
             // m_w * s_a of blocks b - 1 (k = 0..5, lanes 0-31) and b (k = 8..13, lanes
             // 32-63) as bf16 partial products, one bf16 MFMA
@@ -299,24 +293,18 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
             oh[t][BB >> 1] = (int)v;
         }
     }
-#if I8_Q41_BF16
-    int4v wp[F];  // Q4_1: d_w of block BB as its bf16-part operand (zero in lanes 32-63, as wd)
+    int4v wp[F];  // W_Q4_1B: d_w of block BB as its bf16-part operand (zero in lanes 32-63, as wd)
     if constexpr (C::BFS) {
 #pragma unroll
         for (int f = 0; f < F; f++) wp[f] = i8_wparts(wd[f][BB]);
     }
-#endif
     auto ddmfma = [&](int f, int t) {
         if constexpr (WT == W_Q4_0) {
             return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ws[f]),
                                                           __builtin_bit_cast(half8, oh[t]), zf, 0, 0, 0);
         } else if constexpr (C::BFS) {
-#if I8_Q41_BF16
             return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wp[f]),
                                                            __builtin_bit_cast(bf16x8, cur.dp[t]), zf, 0, 0, 0);
-#else
-            return zf;
-#endif
         } else {
             return __builtin_amdgcn_mfma_f32_32x32x2f32(wd[f][BB], cur.da[t], zf, 0, 0, 0);
         }
@@ -348,7 +336,7 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
         for (int i = 0; i < 16; i++) {
 #if I8_Q41_GENERIC
             float v;
-            if constexpr (WT == W_Q4_1)
+            if constexpr (wt_q41(WT))
                 v = acc[p / T][p % T][i] + __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], ms[p / T][p % T][i]);
             else
                 v = __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], acc[p / T][p % T][i]);
@@ -377,8 +365,8 @@ template <int WT, int NT, int BM, int F, int T, bool PIPE = true, typename Hook 
 __device__ __forceinline__ void i8_mainloop(const GemmArgs &g, int64_t m0, int ft0, int tt0, int64_t m0n, int ft0n,
                                             char *smem, I8Pipe<WT, NT, BM, F, AH> &pp, float16v (&acc)[F][T],
                                             const Hook &hook = Hook()) {
-    constexpr bool Q1 = WT == W_Q4_1;
-    using C = I8Chunk<BM, Q1>;
+    constexpr bool Q1 = wt_q41(WT);
+    using C = I8Chunk<BM, Q1, WT == W_Q4_1B>;
     const int lane = threadIdx.x & 63, hh = lane >> 5;
     const int nkb = g.K >> 5, nch = g.K / I8_KC;
     const float4v z4 = {0.f, 0.f, 0.f, 0.f};
@@ -497,7 +485,7 @@ struct I8ResRing {
         if (c < nch) {
 #pragma unroll
             for (int f = 0; f < F; f++) {
-                if constexpr (WT == W_Q4_1) {
+                if constexpr (wt_q41(WT)) {
                     wdr[f] = i8_wvec(g.Wi.d, nkb, ft0 + f, c);
                     wmr[f] = i8_wvec(g.Wi.m, nkb, ft0 + f, c);
                 } else {
@@ -517,8 +505,8 @@ struct I8ResRing {
 template <int WT, int BM, int F, int T, int AH>
 __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
                                                      float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn) {
-    constexpr bool Q1 = WT == W_Q4_1;
-    using C = I8Chunk<BM, Q1>;
+    constexpr bool Q1 = wt_q41(WT);
+    using C = I8Chunk<BM, Q1, WT == W_Q4_1B>;
     const int lane = threadIdx.x & 63, hh = lane >> 5;
     const int nch = g.K / I8_KC;
     const float4v z4 = {0.f, 0.f, 0.f, 0.f};

@@ -26,6 +26,11 @@ namespace bertamd {
 //   W_F32 -> f32, W_F16 -> fp16 (RNE), W_Q4_0 -> Q8_0 (int8 + fp16 d),
 //   W_Q4_1 -> Q8_1 (int8 + f32 d)
 enum WType : int { W_F32 = 0, W_F16 = 1, W_Q4_0 = 2, W_Q4_1 = 3 };
+// gemm_i8.hip only: Q4_1 with its per-block scale products d_w * d_a and
+// m_w * s_a on the bf16 MFMA as exact partial products (i8_core.h i8_aparts),
+// instead of the f32 MFMA; the same weights and activations as W_Q4_1
+constexpr int W_Q4_1B = 4;
+__host__ __device__ constexpr bool wt_q41(int wt) { return wt == W_Q4_1 || wt == W_Q4_1B; }
 
 struct ActPtr {
     void *q = nullptr;  // int8 [M][K] | fp16 [M][K] | f32 [M][K]

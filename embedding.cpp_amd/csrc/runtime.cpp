@@ -258,6 +258,9 @@ struct bert_ctx {
     std::vector<std::unique_ptr<Replica>> reps;
     // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
     bool i8_qkv = false, i8_o = false, i8_down = false, i8_up = false;
+    // Q4_1 int8 GEMMs: scale products on the bf16 MFMA (kernels.h W_Q4_1B) or
+    // the f32 MFMA (load option "q41bf")
+    bool q41bf = false;
     // the fused QKV + attention kernel's form, fixed at load: 1 or 2 = the
     // head-pair kernel with that many 192-feature units per main loop (the tile
     // grouping of its QKV weight copy), 0 = the producer / consumer kernel on an
@@ -706,6 +709,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
     const HParams &hp = ctx->hp;
     Workspace &w = ln.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
+    const int wt8 = (wt == W_Q4_1 && ctx->q41bf) ? W_Q4_1B : wt;  // the int8 GEMMs' weight form
     if (!fused_qkv_attn && row0 != 0) {
         set_err("internal: unfused attention with a row split");
         return false;
@@ -744,7 +748,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
         } else if (ctx->i8_qkv) {  // the int8 QKV of the producer / consumer kernel, unfused
             q.Wi = L.qkv8;
-            LAUNCH_OK("gemm_qkv", launch_gemm_i8(wt, EPI_QKV, q, (int)rows, st));
+            LAUNCH_OK("gemm_qkv", launch_gemm_i8(wt8, EPI_QKV, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
         } else {
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
@@ -764,9 +768,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         if (ctx->i8_o) {
             o.Wi = L.o8;
             if (E == 384) {
-                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt, EPI_LN, o, (int)rows, st));
+                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt8, EPI_LN, o, (int)rows, st));
             } else {
-                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt, EPI_RESID, o, (int)rows, st));
+                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt8, EPI_RESID, o, (int)rows, st));
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
@@ -799,7 +803,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         dn.eps = hp.eps;
         if (ctx->i8_up) {
             u.Wi = L.up8;
-            LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt, EPI_GELU_ACT, u, (int)rows, st));
+            LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt8, EPI_GELU_ACT, u, (int)rows, st));
         } else {
             LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)rows, st));
         }
@@ -807,9 +811,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         if (ctx->i8_down) {
             dn.Wi = L.down8;
             if (E == 384) {
-                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt, EPI_LN, dn, (int)rows, st));
+                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt8, EPI_LN, dn, (int)rows, st));
             } else {
-                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt, EPI_RESID, dn, (int)rows, st));
+                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt8, EPI_RESID, dn, (int)rows, st));
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
@@ -1234,7 +1238,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // fused kernel's weight grouping); every bert_amd_set_option key is accepted
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
-    static const char *keys[] = {"i8", "qkva_ntw", "split", "pack", "fuse_min", "unfused",
+    static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused",
                                  "encode_lanes", "encode_merge", "encode_merge_rows"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
@@ -1275,6 +1279,12 @@ bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
                 return false;
             }
             ctx->qkva_ntw = (int)v;
+        } else if (p.first == "q41bf") {
+            if (v < 0 || v > 1) {
+                set_err("bert_amd option q41bf: must be 0 or 1");
+                return false;
+            }
+            ctx->q41bf = v != 0;
         } else if (apply_option(ctx, p.first, (int32_t)v) != 0) {
             return false;
         }
@@ -2183,7 +2193,8 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
         {"split", ctx->split}, {"pack", ctx->pack}, {"fuse_min", ctx->fuse_min}, {"unfused", ctx->unfused},
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
-        {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down}};
+        {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
+        {"q41bf", ctx->q41bf}};
     for (const auto &o : opts)
         if (k == o.first) {
             *value = o.second;

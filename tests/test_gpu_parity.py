@@ -228,6 +228,44 @@ def test_int8_gemm_path_golden(case, mode, model_dir):
     assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
 
 
+@pytest.mark.parametrize("case", ["minilm_q4_1", "c5_bge_q4_1_l2", "c5_bge_q4_1_l2_short"])
+def test_q41_bf16_scale_products(case, model_dir):
+    """Q4_1 on the int8 GEMMs with the per-block scale products d_w * d_a and
+    m_w * s_a on the bf16 MFMA as exact partial products (load option
+    q41bf=1, kernels.h W_Q4_1B) instead of the f32 MFMA: every projection on
+    it (i8=all), the golden fixtures within the bound, bitwise deterministic,
+    and within the north-star bar of the f32-MFMA form."""
+    meta, toks, want = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    mb = bertlib.BertModel(p, options={"i8": "all", "q41bf": 1})
+    mf = bertlib.BertModel(p, options={"i8": "all", "q41bf": 0})
+    try:
+        assert mb.get_option("q41bf") == 1 and mf.get_option("q41bf") == 0
+        got = mb.eval_batch(toks)
+        assert np.array_equal(got, mb.eval_batch(toks))
+        ref = mf.eval_batch(toks)
+    finally:
+        mb.close()
+        mf.close()
+    c = cos(got, want)
+    print(f"q41bf {case}: 1-cos vs oracle max {1 - c.min():.2e}; vs the f32-MFMA form {1 - cos(got, ref).min():.2e}")
+    assert np.all(1 - c <= parity_bound(meta)), (case, 1 - c)
+    assert cos(got, ref).min() >= COS_TOL
+
+
+def test_bf16_split_scale_product_probe():
+    """tools/mfma_bf16_split_probe.hip: how v_mfma_f32_32x32x16_bf16 rounds a
+    sum of six exact bf16 partial products (the q41bf scale products) against
+    RN(d_w * d_a) and RN(c + d_w * d_a); recorded."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "mfma_bf16_split_probe")
+    assert os.path.exists(exe), "build/mfma_bf16_split_probe missing: run make"
+    out = subprocess.run([exe, "16384"], capture_output=True, text=True, timeout=120).stdout
+    print(out)
+    _record("bf16_split_probe.txt.json", {"stdout": out})
+    assert "product alone:" in out and "with accumulator:" in out
+
+
 def test_batch_invariance_and_determinism(model_dir):
     p, m = get_model(model_dir, "minilm", "q4_0")
     toks = [sentence(i, n, 30522) for i, n in enumerate([5, 128, 64, 17, 512, 128])]
