@@ -415,6 +415,147 @@ __global__ __launch_bounds__(768) void i8_qkv_kernel(GemmArgs g, int n_mtiles, i
 }
 
 // ---------------------------------------------------------------------------
+// Small batches (one server sentence: 128 padded rows).  The batch kernels
+// give a workgroup whole 64-row x 384-column tiles over the full K, so a
+// 128-row batch runs on 2-6 CUs and each kernel lasts one tile's walk of K
+// (FFN-down: ~36 us).  Here a workgroup owns 32 rows x 32 NW columns, one
+// f-tile per wave (4 N / (32 NW) workgroups at 128 rows), through the same
+// chunk-staged main loop and block step (i8_mainloop / i8_block): every sum is
+// the batch kernels' bit for bit, so a sentence's embedding does not depend on
+// the batch it came in.  Epilogues: EPI_QKV and EPI_GELU_ACT as the batch
+// kernels (the GELU table read from L2 instead of LDS: the same entries);
+// EPI_RESID X = (b + W.x) + X, for EPI_LN followed by i8_ln384_rows_kernel.
+#ifndef I8_SK_WAVES
+#define I8_SK_WAVES 2
+#endif
+
+template <int WT, int EPI, int NW>
+__global__ __launch_bounds__(NW * 64) void i8_small_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
+    constexpr int NT = NW * 64, BM = 32, F = 1, T = 1;
+    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
+    __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+    const int nwg = n_mtiles * n_ntiles;
+    if ((int)blockIdx.x >= nwg) return;
+    const int lin = xcd_linear(blockIdx.x, nwg);
+    const int mt = lin / n_ntiles, nt = lin - mt * n_ntiles;
+    const int64_t m0 = (int64_t)mt * BM;
+    const int ft0 = nt * NW + wv;
+    I8Pipe<WT, NT, BM, F> pp;
+    pp.prime(g, m0, ft0);
+    float16v acc[F][T];
+    i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0, ft0, smem, pp, acc);  // (the "next tile" is this one)
+    const int64_t row = m0 + l32;
+    const int f0 = 32 * ft0 + 16 * hh;
+    float bias[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
+    }
+    if constexpr (EPI == EPI_QKV) {  // i8_qkv_kernel's epilogue
+        const int E = g.N / 3, D = g.head_dim;
+        const int hd = f0 / (3 * D), part = (f0 - hd * 3 * D) / D, dd = f0 - hd * 3 * D - part * D;
+        half8 hv[2], lv[2];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const float y = bias[i] + acc[0][0][i];
+            const _Float16 yh = (_Float16)y;
+            hv[i >> 3][i & 7] = yh;
+            lv[i >> 3][i & 7] = (_Float16)(y - (float)yh);
+        }
+        if (part < 2) {
+            const int64_t o = row * (2 * E) + part * E + hd * D + dd;
+            *(half8 *)(g.qk_hi + o) = hv[0];
+            *(half8 *)(g.qk_hi + o + 8) = hv[1];
+            *(half8 *)(g.qk_lo + o) = lv[0];
+            *(half8 *)(g.qk_lo + o + 8) = lv[1];
+        } else {
+            const int64_t c0 = hd * D + dd;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                ((_Float16 *)g.vt_hi)[(c0 + i) * g.ldv + row] = hv[i >> 3][i & 7];
+                ((_Float16 *)g.vt_lo)[(c0 + i) * g.ldv + row] = lv[i >> 3][i & 7];
+            }
+        }
+    } else if constexpr (EPI == EPI_GELU_ACT) {  // i8_up_gelu_kernel's epilogue
+        const uint16_t *gt = g.gelu.full;
+        const float xlo = h2f((uint16_t)(0x8000 | g.gelu.neg_n));
+        float y[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) y[i] = h2f(gt[f2h(fmaxf(bias[i] + acc[0][0][i], xlo))]);
+        i8_store_q8_half<WT>(g.out_act, g.N, row, ft0, hh, y);
+    } else {  // EPI_RESID: i8_resid_kernel's / i8_ln384_kernel's v = (b + W.x) + x
+        float4v *xp = (float4v *)(g.X + row * g.N + f0);
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const float4v x4 = xp[qq];
+            float4v o;
+#pragma unroll
+            for (int j = 0; j < 4; j++) o[j] = (bias[4 * qq + j] + acc[0][0][4 * qq + j]) + x4[j];
+            xp[qq] = o;
+        }
+    }
+}
+
+// LayerNorm of 384-wide rows after i8_small_kernel's residual: i8_ln384_kernel's
+// epilogue with its reduction order — lane (w = l & 31 < 12, hh = l >> 5) holds
+// columns 32 w + 16 hh .. + 15 (its wave w / lane half hh there); double sums
+// over the 16 in order, the lane-half pair, then the twelve in order.  One wave
+// per row.
+template <int WT>
+__global__ __launch_bounds__(256) void i8_ln384_rows_kernel(GemmArgs g, int Mpad) {
+    const int lane = threadIdx.x & 63, w = lane & 31, hh = lane >> 5;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= Mpad) return;
+    const bool on = w < 12;
+    const int col = 32 * (on ? w : 0) + 16 * hh;
+    float *xr = g.X + row * 384 + col;
+    float v[16];
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) {
+        const float4v x4 = *(const float4v *)(xr + 4 * qq);
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[4 * qq + j] = x4[j];
+    }
+    auto row_sum = [&](double s) {  // s: this lane's 16-term sum; the row total in every lane
+        s += __shfl_xor(s, 32);
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < 12; k++) tot += __shfl(s, k);
+        return tot;
+    };
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) s += (double)v[i];
+    const float mean = (float)(row_sum(s) / 384);
+    double s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        v[i] = v[i] - mean;
+        s2 += (double)(v[i] * v[i]);
+    }
+    const float var = (float)(row_sum(s2) / 384);
+    const float scale = 1.0f / sqrtf(var + g.eps);
+    if (!on) return;  // both lane halves of a column block leave together (i8_store_q8_half pairs them)
+    float y[16];
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) {
+        const float4v w4 = *(const float4v *)(g.ln_w + col + 4 * qq);
+        const float4v b4 = *(const float4v *)(g.ln_b + col + 4 * qq);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            float z = v[4 * qq + j] * scale;
+            z = w4[j] * z;
+            y[4 * qq + j] = z + b4[j];
+        }
+        *(float4v *)(xr + 4 * qq) = float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
+    }
+    i8_store_q8_half<WT>(g.out_act, 384, row, w, hh, y);
+}
+
+// ---------------------------------------------------------------------------
 static int n_cus_i8() {
     static int n = [] {
         int dev = 0, c = 0;
@@ -466,6 +607,42 @@ hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipSt
         case W_Q4_0: return i8_gemm_t<W_Q4_0>(epi, a, Mpad, s);
         case W_Q4_1: return i8_gemm_t<W_Q4_1>(epi, a, Mpad, s);
         case W_Q4_1B: return i8_gemm_t<W_Q4_1B>(epi, a, Mpad, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int WT>
+static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
+    constexpr int NW = I8_SK_WAVES;
+    if (a.N % (32 * NW) || Mpad % 32) return hipErrorInvalidValue;
+    const int mt = Mpad / 32, nt = a.N / (32 * NW);
+    const dim3 grid(mt * nt), block(NW * 64);
+    switch (epi) {
+        case EPI_QKV:
+            if (a.head_dim <= 0 || a.head_dim % 16 || (a.N / 3) % a.head_dim) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((i8_small_kernel<WT, EPI_QKV, NW>), grid, block, 0, s, a, mt, nt);
+            break;
+        case EPI_GELU_ACT: hipLaunchKernelGGL((i8_small_kernel<WT, EPI_GELU_ACT, NW>), grid, block, 0, s, a, mt, nt); break;
+        case EPI_RESID: hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW>), grid, block, 0, s, a, mt, nt); break;
+        case EPI_LN: {
+            if (a.N != 384) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW>), grid, block, 0, s, a, mt, nt);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((i8_ln384_rows_kernel<WT>), dim3(Mpad / 4), dim3(256), 0, s, a, Mpad);
+            break;
+        }
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_gemm_i8_small(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
+    if (!i8_gemm_supported(epi, a.N, a.K) || Mpad % 128) return hipErrorInvalidValue;
+    switch (wtype) {
+        case W_Q4_0: return i8_small_t<W_Q4_0>(epi, a, Mpad, s);
+        case W_Q4_1: return i8_small_t<W_Q4_1>(epi, a, Mpad, s);
+        case W_Q4_1B: return i8_small_t<W_Q4_1B>(epi, a, Mpad, s);
     }
     return hipErrorInvalidValue;
 }

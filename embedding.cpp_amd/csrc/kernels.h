@@ -189,5 +189,8 @@ bool i8_gemm_supported(int epi, int N, int K);
 hipError_t stamps_set(unsigned long long *buf, int nblk);  // development stamp builds (kernels.hip)
 #endif
 hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
+// the same GEMMs (bitwise) in 32-row tiles for small batches (EPI_LN: residual
+// kernel + a LayerNorm kernel in i8_ln384_kernel's reduction order)
+hipError_t launch_gemm_i8_small(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
 
 }  // namespace bertamd

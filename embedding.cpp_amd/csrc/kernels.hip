@@ -2176,6 +2176,12 @@ hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s) 
 // 128-row one (tools/gemm_bench: 162 us either way at M = 131072), so they are
 // used when they take fewer rounds of n_cus workgroups than twice the 128-row
 // count — i.e. when 128-row tiles would leave the last round mostly empty.
+// (and 32-row tiles for small batches, one server sentence = 128 rows: a row
+// tile's latency, not the chip, bounds those; the per-row sums do not depend on
+// the tile height)
+#ifndef LN_SMALL_ROWS
+#define LN_SMALL_ROWS 512
+#endif
 static bool ln_half_rows(int Mpad) {
     const int c = n_cus(), r128 = (Mpad / 128 + c - 1) / c, r64 = (Mpad / 64 + c - 1) / c;
     return r64 < 2 * r128;
@@ -2206,8 +2212,9 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
             return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)
                                   : gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
         if (epi == EPI_LN && a.N == 384)
-            return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
-                                      : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
+            return Mpad <= LN_SMALL_ROWS ? gemm_t<WT, EPI_LN, 384, 12, 32>(a, Mpad, s)
+                   : ln_half_rows(Mpad)  ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
+                                         : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
     } else if constexpr (WT == W_F16) {
         // tools/gemm_bench (e5 shapes): 12-wave 384-column tiles win by 1.3-1.8x over
@@ -2218,8 +2225,9 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
                                   : gemm_t<WT, EPI_GELU_ACT, 256, 4, 64>(a, Mpad, s);
         switch (a.N) {
             case 384:
-                return ln_half_rows(Mpad) ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
-                                          : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
+                return Mpad <= LN_SMALL_ROWS ? gemm_t<WT, EPI_LN, 384, 12, 32>(a, Mpad, s)
+                       : ln_half_rows(Mpad)  ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
+                                             : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
             case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);
             case 1024: return gemm_t<WT, EPI_LN, 1024, 8, 32>(a, Mpad, s);
         }

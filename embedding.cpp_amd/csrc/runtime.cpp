@@ -277,6 +277,10 @@ struct bert_ctx {
     // pair, whose GEMM and attention spread a sentence over many workgroups
     int split = 1, pack = -1, fuse_min = 48;
     bool unfused = false;
+    // batches of at most small_rows padded rows run the int8 GEMMs in their
+    // 32-row-tile form (gemm_i8.hip i8_small_kernel: the same sums, spread over
+    // many more workgroups; a one-sentence batch is 128 rows); 0 = never
+    int small_rows = 2048;
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
     // merging only up to encode_merge_rows sentences (slices that large already
@@ -710,6 +714,11 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
     Workspace &w = ln.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
     const int wt8 = (wt == W_Q4_1 && ctx->q41bf) ? W_Q4_1B : wt;  // the int8 GEMMs' weight form
+    // small batches: the int8 GEMMs in 32-row tiles (bitwise the same results)
+    const bool small = rows <= ctx->small_rows;
+    auto gemm_i8 = [&](int epi, const GemmArgs &a) {
+        return small ? launch_gemm_i8_small(wt8, epi, a, (int)rows, st) : launch_gemm_i8(wt8, epi, a, (int)rows, st);
+    };
     if (!fused_qkv_attn && row0 != 0) {
         set_err("internal: unfused attention with a row split");
         return false;
@@ -748,7 +757,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
         } else if (ctx->i8_qkv) {  // the int8 QKV of the producer / consumer kernel, unfused
             q.Wi = L.qkv8;
-            LAUNCH_OK("gemm_qkv", launch_gemm_i8(wt8, EPI_QKV, q, (int)rows, st));
+            LAUNCH_OK("gemm_qkv", gemm_i8(EPI_QKV, q));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
         } else {
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
@@ -768,9 +777,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         if (ctx->i8_o) {
             o.Wi = L.o8;
             if (E == 384) {
-                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt8, EPI_LN, o, (int)rows, st));
+                LAUNCH_OK("gemm_o_ln", gemm_i8(EPI_LN, o));
             } else {
-                LAUNCH_OK("gemm_o_ln", launch_gemm_i8(wt8, EPI_RESID, o, (int)rows, st));
+                LAUNCH_OK("gemm_o_ln", gemm_i8(EPI_RESID, o));
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
@@ -803,7 +812,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         dn.eps = hp.eps;
         if (ctx->i8_up) {
             u.Wi = L.up8;
-            LAUNCH_OK("gemm_up_gelu", launch_gemm_i8(wt8, EPI_GELU_ACT, u, (int)rows, st));
+            LAUNCH_OK("gemm_up_gelu", gemm_i8(EPI_GELU_ACT, u));
         } else {
             LAUNCH_OK("gemm_up_gelu", launch_gemm(wt, EPI_GELU_ACT, 0, u, (int)rows, st));
         }
@@ -811,9 +820,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         if (ctx->i8_down) {
             dn.Wi = L.down8;
             if (E == 384) {
-                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt8, EPI_LN, dn, (int)rows, st));
+                LAUNCH_OK("gemm_down_ln", gemm_i8(EPI_LN, dn));
             } else {
-                LAUNCH_OK("gemm_down_ln", launch_gemm_i8(wt8, EPI_RESID, dn, (int)rows, st));
+                LAUNCH_OK("gemm_down_ln", gemm_i8(EPI_RESID, dn));
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
             }
         } else if (ln_fused) {
@@ -1221,6 +1230,9 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         ctx->fuse_min = value;
     } else if (k == "unfused") {
         ctx->unfused = value != 0;
+    } else if (k == "small_rows") {
+        if (need(value >= 0, "must be >= 0")) return -2;
+        ctx->small_rows = value;
     } else if (k == "encode_lanes" || k == "encode_merge" || k == "encode_merge_rows") {
         if (need(value >= 1, "must be >= 1")) return -2;
         (k == "encode_lanes" ? ctx->encode_lanes : k == "encode_merge" ? ctx->encode_merge : ctx->encode_merge_rows) = value;
@@ -1238,7 +1250,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // fused kernel's weight grouping); every bert_amd_set_option key is accepted
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
-    static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused",
+    static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows",
                                  "encode_lanes", "encode_merge", "encode_merge_rows"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
@@ -2191,6 +2203,7 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
     const std::string k = key;
     const std::pair<const char *, int32_t> opts[] = {
         {"split", ctx->split}, {"pack", ctx->pack}, {"fuse_min", ctx->fuse_min}, {"unfused", ctx->unfused},
+        {"small_rows", ctx->small_rows},
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},

@@ -786,6 +786,45 @@ def test_small_batches_unfused_bitwise_fused(shape, ftype, model_dir):
     assert np.array_equal(m.eval(toks[5]), fused[5])
 
 
+@pytest.mark.parametrize("shape,ftype,n_layer,opts", [
+    ("minilm", "q4_0", None, {}),
+    ("minilm", "q4_0", None, {"i8": "all"}),
+    ("minilm", "q4_1", None, {"i8": "all"}),
+    ("minilm", "q4_1", None, {"i8": "all", "q41bf": 1}),
+    ("bge-large", "q4_1", 2, {"i8": "all"}),
+])
+def test_small_row_tiles_bitwise(shape, ftype, n_layer, opts, model_dir):
+    """Batches of at most small_rows padded rows (one server sentence: 128) run
+    the int8 GEMMs in 32-row tiles (gemm_i8.hip i8_small_kernel, and for
+    n_embd 384 the LayerNorm in i8_ln384_kernel's reduction order) and the
+    split-fp16 LayerNorm GEMM in 32-row tiles: every embedding bitwise the
+    batch kernels' (small_rows 0), alone or in a batch, so a sentence's result
+    does not depend on the batch it came in."""
+    p = ensure_model(model_dir, shape, ftype, 0.05, n_layer)
+    m = bertlib.BertModel(p, options=opts)
+    try:
+        rng = np.random.default_rng(55)
+        vocab = 30522
+        lens = [1, 2, 5, 31, 32, 33, 64, 100, 127, 128, 129, 200, 512]
+        toks = [[101] + rng.integers(1000, vocab, max(n - 2, 0)).tolist() + [102] for n in lens]
+        toks[0] = [101]
+        batches = [[t] for t in toks] + [toks[1:9], [sentence(900 + i, 128, vocab) for i in range(16)]]
+        m.set_option("small_rows", 0)
+        want = [m.eval_batch(b) for b in batches]
+        m.set_option("small_rows", 4096)
+        for b, w in zip(batches, want):
+            got = m.eval_batch(b)
+            bad = [i for i in range(len(b)) if not np.array_equal(got[i], w[i])]
+            assert not bad, (opts, [len(b[i]) for i in bad])
+        assert np.array_equal(m.eval(toks[9]), want[9][0])
+        if ftype == "q4_0":  # (Q4_1: the golden fixtures, with ggml's order-spread bounds)
+            import oracle
+            c = cos(np.concatenate(want[:4]), oracle.Oracle(p).eval_batch(toks[:4], 0))
+            assert c.min() >= COS_TOL, 1 - c
+    finally:
+        m.close()
+
+
 def test_encode_batch_lanes_bitwise(model_dir):
     """bert_encode_batch with many small slices runs them on several lanes
     (workspaces + streams) at once; every embedding equals the one-batch

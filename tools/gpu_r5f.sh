@@ -12,7 +12,7 @@ bash tools/gpu_steps.sh \
   c5_def_all 300 "BERT_AMD_I8=all python3 bench.py $C5 > gpurun_out/c5_def_all.json" \
   c5_bf_all 300 "BERT_AMD_I8=all BERT_AMD_Q41BF=1 python3 bench.py $C5 > gpurun_out/c5_bf_all.json" \
   q41tests 300 "$T tests/test_gpu_parity.py -k 'q41_bf16 or bf16_split'" \
-  bench 300 "python3 bench.py --steps 20 --warmup 5 --cpu-sample 64 > gpurun_out/r05b_bench.json" \
+  \
   diag_def 500 "BERT_AMD_PARITY_DIAG=1 $T tests/test_gpu_parity.py -k attention_operand_form tests/test_layer_parity.py -k c5" \
   save 30 "mkdir -p gpurun_out/diag_def && cp gpurun_out/layer_parity_*.json gpurun_out/attnform_*.json gpurun_out/diag_def/" \
   diag_gen 500 "BERT_AMD_PARITY_DIAG=1 BERT_AMD_LIB=build/var/q41gen/libbert.so $T tests/test_gpu_parity.py -k 'attention_operand_form and c5' tests/test_layer_parity.py -k c5"
