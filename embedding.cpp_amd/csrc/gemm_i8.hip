@@ -154,11 +154,12 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
     int64_t m0n = (int64_t)xcd_linear(blockIdx.x, n_mtiles) * BM;
     I8Pipe<WT, NT, BM, F, I8_LN_AHEAD> pp;
     pp.prime(g, m0n, ft0);
-    // wave w's piece k: LDS chunks 64 (8 w + k) .. + 63 of xs, i.e. lane l holds
-    // chunk j = 64 (8 w + k) + l = (row r, column chunk cs ^ (r & 15)) of the tile
+    // wave w's piece k: LDS chunks 64 (P w + k) .. + 63 of xs (P = PIECES), i.e.
+    // lane l holds chunk j = 64 (P w + k) + l = (row r, column chunk cs ^ (r & 15))
     constexpr int PIECES = XCH / NT;  // 1 KiB pieces per wave
+    static_assert(PIECES * NT == XCH, "whole pieces per wave");
     auto piece_off = [&](int k, int &j0) {
-        j0 = 64 * (8 * wv + k);
+        j0 = 64 * (PIECES * wv + k);
         const int j = j0 + lane, r = j / 96, cs = j - 96 * r;
         return r * NCOL + 4 * (cs ^ (r & 15));
     };
@@ -419,21 +420,33 @@ __global__ __launch_bounds__(768) void i8_qkv_kernel(GemmArgs g, int n_mtiles, i
 // give a workgroup whole 64-row x 384-column tiles over the full K, so a
 // 128-row batch runs on 2-6 CUs and each kernel lasts one tile's walk of K
 // (FFN-down: ~36 us).  Here a workgroup owns 32 rows x 32 NW columns, one
-// f-tile per wave (4 N / (32 NW) workgroups at 128 rows), through the same
-// chunk-staged main loop and block step (i8_mainloop / i8_block): every sum is
-// the batch kernels' bit for bit, so a sentence's embedding does not depend on
-// the batch it came in.  Epilogues: EPI_QKV and EPI_GELU_ACT as the batch
+// f-tile per wave (4 N / (32 NW) workgroups at 128 rows), and each wave's
+// walk of K is latency-bound, not issue-bound: so the operands are fetched a
+// whole segment (SEG chunks = 4 SEG quant blocks) ahead — the A chunks of the
+// next segment into registers while this one is computed (one barrier per
+// segment), the weight fragments through a 4 SEG-slot register ring refilled
+// 4 SEG blocks ahead.  The block step is i8_block, in block order: every sum
+// is the batch kernels' bit for bit, so a sentence's embedding does not depend
+// on the batch it came in.  Epilogues: EPI_QKV and EPI_GELU_ACT as the batch
 // kernels (the GELU table read from L2 instead of LDS: the same entries);
 // EPI_RESID X = (b + W.x) + X, for EPI_LN followed by i8_ln384_rows_kernel.
+// (A 12-wave form with the LayerNorm in its epilogue — whole rows per
+// workgroup, 4 workgroups for one sentence — measured 24 us against 20 us for
+// the two kernels: at 4 CUs the block steps are issue-bound.)
 #ifndef I8_SK_WAVES
 #define I8_SK_WAVES 2
 #endif
+#ifndef I8_SK_SEG
+#define I8_SK_SEG 4
+#endif
 
-template <int WT, int EPI, int NW>
+template <int WT, int EPI, int NW, int SEG>
 __global__ __launch_bounds__(NW * 64) void i8_small_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
-    constexpr int NT = NW * 64, BM = 32, F = 1, T = 1;
-    using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
-    __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
+    constexpr int NT = NW * 64, BM = 32, F = 1, T = 1, NS = 4 * SEG;  // NS: blocks per segment
+    constexpr bool Q1 = wt_q41(WT);
+    using C = I8Chunk<BM, Q1, WT == W_Q4_1B>;
+    constexpr int IT = (4 * BM + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) char smem[2 * SEG * C::BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int nwg = n_mtiles * n_ntiles;
     if ((int)blockIdx.x >= nwg) return;
@@ -441,10 +454,93 @@ __global__ __launch_bounds__(NW * 64) void i8_small_kernel(GemmArgs g, int n_mti
     const int mt = lin / n_ntiles, nt = lin - mt * n_ntiles;
     const int64_t m0 = (int64_t)mt * BM;
     const int ft0 = nt * NW + wv;
-    I8Pipe<WT, NT, BM, F> pp;
-    pp.prime(g, m0, ft0);
+    const int K = g.K, nkb = K >> 5, nch = K / I8_KC, nseg = (nch + SEG - 1) / SEG;
+
+    int4v wf[NS][F];                                    // weight ring: block b in slot b % NS
+    uint2 wr[2][SEG][F];                                // Q4_0 d_w (this / next segment)
+    float4v wdr[2][SEG][F], wmr[2][SEG][F];             // Q4_1 d_w, m_w
+    I8Items<IT> st[SEG];                                // the next segment's A chunks
+    auto load_scales = [&](int set, int sg) {
+#pragma unroll
+        for (int cc = 0; cc < SEG; cc++) {
+            const int c = sg * SEG + cc;
+            if (c < nch) {
+                if constexpr (Q1) {
+                    wdr[set][cc][0] = i8_wvec(g.Wi.d, nkb, ft0, c);
+                    wmr[set][cc][0] = i8_wvec(g.Wi.m, nkb, ft0, c);
+                } else {
+                    wr[set][cc][0] = ((const uint2 *)g.Wi.dh)[((int64_t)ft0 * (nkb >> 2) + c) * 32 + (lane & 31)];
+                }
+            }
+        }
+    };
+    auto load_a = [&](int sg) {
+#pragma unroll
+        for (int cc = 0; cc < SEG; cc++)
+            if (sg * SEG + cc < nch) i8_stage_load<WT, BM, NT>(st[cc], g.A, K, m0, (sg * SEG + cc) * I8_KC);
+    };
+    auto store_a = [&](int sg) {
+#pragma unroll
+        for (int cc = 0; cc < SEG; cc++)
+            if (sg * SEG + cc < nch) i8_stage_store<WT, BM, NT>(st[cc], smem + ((sg & 1) * SEG + cc) * C::BYTES);
+    };
+#pragma unroll
+    for (int j = 0; j < NS; j++)
+        if (j < nkb) wf[j][0] = i8_wq(g.Wi, nkb, ft0, j);
+    load_scales(0, 0);
+    load_a(0);
+    store_a(0);
+    __syncthreads();
+
     float16v acc[F][T];
-    i8_mainloop<WT, NT, BM, F, T>(g, m0, ft0, 0, m0, ft0, smem, pp, acc);  // (the "next tile" is this one)
+    acc[0][0] = float16v{};
+    const float4v z4 = {0.f, 0.f, 0.f, 0.f};
+    for (int sg = 0; sg < nseg; sg++) {
+        const bool more = sg + 1 < nseg;
+        if (more) {
+            load_scales(1, sg + 1);
+            load_a(sg + 1);
+        }
+#pragma unroll
+        for (int cc = 0; cc < SEG; cc++) {
+            const int c = sg * SEG + cc;
+            if (c < nch) {
+                const char *buf = smem + ((sg & 1) * SEG + cc) * C::BYTES;
+                int4v ws[F];
+                float4v wd[F], wm[F];
+                if constexpr (Q1) {
+                    wd[0] = hh ? z4 : wdr[0][cc][0];  // i8_mainloop's wscale_use
+                    wm[0] = wmr[0][cc][0];
+                } else {
+                    ws[0] = int4v{(int)wr[0][cc][0].x, (int)wr[0][cc][0].y, (int)wr[0][cc][0].x, (int)wr[0][cc][0].y};
+                }
+                auto refill = [&](int j) {  // slot 4 cc + j: block 4 c + j done, block 4 c + j + NS next
+                    const int b = 4 * c + j + NS;
+                    if (b < nkb) wf[4 * cc + j][0] = i8_wq(g.Wi, nkb, ft0, b);
+                };
+                I8AOps<T> a0, a1;
+                i8_aops<WT, BM, T, 0>(a0, buf, 0);
+                i8_block<WT, BM, F, T, 0, true>(buf, 0, wf[4 * cc + 0], ws, wd, wm, a0, a1, acc);
+                refill(0);
+                i8_block<WT, BM, F, T, 1, true>(buf, 0, wf[4 * cc + 1], ws, wd, wm, a1, a0, acc);
+                refill(1);
+                i8_block<WT, BM, F, T, 2, true>(buf, 0, wf[4 * cc + 2], ws, wd, wm, a0, a1, acc);
+                refill(2);
+                i8_block<WT, BM, F, T, 3, true>(buf, 0, wf[4 * cc + 3], ws, wd, wm, a1, a0, acc);
+                refill(3);
+            }
+        }
+        if (more) {
+            store_a(sg + 1);
+#pragma unroll
+            for (int cc = 0; cc < SEG; cc++) {
+                wr[0][cc][0] = wr[1][cc][0];
+                wdr[0][cc][0] = wdr[1][cc][0];
+                wmr[0][cc][0] = wmr[1][cc][0];
+            }
+        }
+        __syncthreads();
+    }
     const int64_t row = m0 + l32;
     const int f0 = 32 * ft0 + 16 * hh;
     float bias[16];
@@ -613,21 +709,22 @@ hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipSt
 
 template <int WT>
 static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
-    constexpr int NW = I8_SK_WAVES;
-    if (a.N % (32 * NW) || Mpad % 32) return hipErrorInvalidValue;
-    const int mt = Mpad / 32, nt = a.N / (32 * NW);
+    constexpr int NW = I8_SK_WAVES, SEG = I8_SK_SEG;
+    if (Mpad % 32) return hipErrorInvalidValue;
+    const int mt = Mpad / 32;
+    if (a.N % (32 * NW) || (epi == EPI_LN && a.N != 384)) return hipErrorInvalidValue;
+    const int nt = a.N / (32 * NW);
     const dim3 grid(mt * nt), block(NW * 64);
     switch (epi) {
         case EPI_QKV:
             if (a.head_dim <= 0 || a.head_dim % 16 || (a.N / 3) % a.head_dim) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((i8_small_kernel<WT, EPI_QKV, NW>), grid, block, 0, s, a, mt, nt);
+            hipLaunchKernelGGL((i8_small_kernel<WT, EPI_QKV, NW, SEG>), grid, block, 0, s, a, mt, nt);
             break;
-        case EPI_GELU_ACT: hipLaunchKernelGGL((i8_small_kernel<WT, EPI_GELU_ACT, NW>), grid, block, 0, s, a, mt, nt); break;
-        case EPI_RESID: hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW>), grid, block, 0, s, a, mt, nt); break;
+        case EPI_GELU_ACT: hipLaunchKernelGGL((i8_small_kernel<WT, EPI_GELU_ACT, NW, SEG>), grid, block, 0, s, a, mt, nt); break;
+        case EPI_RESID: hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW, SEG>), grid, block, 0, s, a, mt, nt); break;
         case EPI_LN: {
-            if (a.N != 384) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW>), grid, block, 0, s, a, mt, nt);
-            hipError_t e = hipGetLastError();
+            hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW, SEG>), grid, block, 0, s, a, mt, nt);
+            const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL((i8_ln384_rows_kernel<WT>), dim3(Mpad / 4), dim3(256), 0, s, a, Mpad);
             break;

@@ -187,7 +187,8 @@ __device__ __forceinline__ void table8(const void *tab, int type, int64_t row, i
 // in double combined quarter -> block (shuffles) -> row (fixed block order).
 // Position of every packed row inside its sentence (positions 0..n-1,
 // bert.cpp:874-878), one workgroup per sentence: embed_ln_kernel then reads
-// it instead of searching the offsets per row.
+// it instead of searching the offsets per row (small batches: no rowpos, the
+// embed kernel searches the offsets itself — one kernel launch less).
 __global__ __launch_bounds__(128) void row_pos_kernel(const int32_t *__restrict__ offsets, int32_t *__restrict__ rowpos) {
     const int s = blockIdx.x, beg = offsets[s], end = offsets[s + 1];
     for (int r = beg + (int)threadIdx.x; r < end; r += 128) rowpos[r] = r - beg;
@@ -205,7 +206,19 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(EmbedArgs a) {
         int tok = -1, pos = 0;
         if (row < a.M) {
             tok = min(max(a.tokens[row], 0), a.n_vocab - 1);  // ids are validated on the host path;
-            pos = min(a.rowpos[row], a.n_pos - 1);              // clamp keeps device-fed ids in bounds
+            int p;
+            if (a.rowpos) {
+                p = a.rowpos[row];
+            } else {  // last sentence s with offsets[s] <= row
+                int lo = 0, hi = a.n_seqs - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (a.offsets[mid] <= row) lo = mid;
+                    else hi = mid - 1;
+                }
+                p = (int)(row - a.offsets[lo]);
+            }
+            pos = min(p, a.n_pos - 1);  // clamp keeps device-fed ids in bounds
         }
         rinfo[2 * tid] = tok;
         rinfo[2 * tid + 1] = pos;
@@ -2151,8 +2164,11 @@ __global__ __launch_bounds__(128) void gather_tokens_kernel(const int32_t *__res
 // ---------------------------------------------------------------------------
 // launchers
 template <int WT>
-static hipError_t embed_t(const EmbedArgs &a, int Mpad, hipStream_t s) {
-    if (a.n_seqs > 0) hipLaunchKernelGGL(row_pos_kernel, dim3(a.n_seqs), dim3(128), 0, s, a.offsets, a.rowpos);
+static hipError_t embed_t(EmbedArgs a, int Mpad, hipStream_t s) {
+    if (a.n_seqs > 64)
+        hipLaunchKernelGGL(row_pos_kernel, dim3(a.n_seqs), dim3(128), 0, s, a.offsets, a.rowpos);
+    else
+        a.rowpos = nullptr;  // embed_ln_kernel searches the offsets
     switch (a.E) {
         case 384: hipLaunchKernelGGL((embed_ln_kernel<WT, 12>), dim3(Mpad / 16), dim3(256), 0, s, a); break;
         case 768: hipLaunchKernelGGL((embed_ln_kernel<WT, 24>), dim3(Mpad / 16), dim3(256), 0, s, a); break;
@@ -2181,6 +2197,9 @@ hipError_t launch_embed(int wtype, const EmbedArgs &a, int Mpad, hipStream_t s) 
 // the tile height)
 #ifndef LN_SMALL_ROWS
 #define LN_SMALL_ROWS 512
+#endif
+#ifndef LN_SMALL_BM
+#define LN_SMALL_BM 16
 #endif
 static bool ln_half_rows(int Mpad) {
     const int c = n_cus(), r128 = (Mpad / 128 + c - 1) / c, r64 = (Mpad / 64 + c - 1) / c;
@@ -2212,7 +2231,7 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
             return a.N % 384 == 0 ? gemm_t<WT, EPI_GELU_ACT, 384, 12, 128>(a, Mpad, s)
                                   : gemm_t<WT, EPI_GELU_ACT, 256, 8, 128>(a, Mpad, s);
         if (epi == EPI_LN && a.N == 384)
-            return Mpad <= LN_SMALL_ROWS ? gemm_t<WT, EPI_LN, 384, 12, 32>(a, Mpad, s)
+            return Mpad <= LN_SMALL_ROWS ? gemm_t<WT, EPI_LN, 384, 12, LN_SMALL_BM>(a, Mpad, s)
                    : ln_half_rows(Mpad)  ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
                                          : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
         if (epi == EPI_RESID) return gemm_t<WT, EPI_RESID, 256, 8, 128>(a, Mpad, s);
@@ -2225,7 +2244,7 @@ static hipError_t gemm_w(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
                                   : gemm_t<WT, EPI_GELU_ACT, 256, 4, 64>(a, Mpad, s);
         switch (a.N) {
             case 384:
-                return Mpad <= LN_SMALL_ROWS ? gemm_t<WT, EPI_LN, 384, 12, 32>(a, Mpad, s)
+                return Mpad <= LN_SMALL_ROWS ? gemm_t<WT, EPI_LN, 384, 12, LN_SMALL_BM>(a, Mpad, s)
                        : ln_half_rows(Mpad)  ? gemm_t<WT, EPI_LN, 384, 12, 64>(a, Mpad, s)
                                              : gemm_t<WT, EPI_LN, 384, 12, 128>(a, Mpad, s);
             case 768: return gemm_t<WT, EPI_LN, 768, 12, 64>(a, Mpad, s);

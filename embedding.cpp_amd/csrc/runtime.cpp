@@ -198,6 +198,7 @@ struct Workspace {
     int32_t *h_tok = nullptr, *h_off = nullptr;
     float *h_out = nullptr;
     int64_t h_cap_rows = 0, h_cap_seqs = 0;
+    uint64_t gen = 0;  // bumped when the device buffers are reallocated (captured graphs hold their addresses)
 };
 
 struct ProfEntry {
@@ -219,6 +220,11 @@ struct Lane {
     // buffers an earlier call on another stream is still reading
     hipEvent_t ev_free = nullptr;
     Workspace ws;
+    // small host batches: the pipeline's launches captured once per batch shape
+    // (the sentences' token offsets) and replayed as one graph launch
+    // (run_host_pipeline); valid for one workspace generation and option state
+    std::map<std::vector<int32_t>, hipGraphExec_t> graphs;
+    uint64_t graphs_ws_gen = 0, graphs_opt_gen = 0;
 };
 
 struct Replica {
@@ -281,6 +287,13 @@ struct bert_ctx {
     // 32-row-tile form (gemm_i8.hip i8_small_kernel: the same sums, spread over
     // many more workgroups; a one-sentence batch is 128 rows); 0 = never
     int small_rows = 2048;
+    // host batches of at most graph_seqs sentences (and fewer than fuse_min, so
+    // that the pipeline makes no host copy) replay a captured HIP graph of their
+    // launches: one launch instead of ~33 per call; 0 = never (default: the
+    // one-sentence call measured 327 us eager, 332 us replayed — the device's
+    // ~4.5 us per dependent kernel bounds it, not the host's launches)
+    int graph_seqs = 0;
+    uint64_t opt_gen = 0;  // bumped by every option change (captured graphs are dropped)
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
     // merging only up to encode_merge_rows sentences (slices that large already
@@ -608,6 +621,7 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
     HIP_OK(hipMemsetAsync(w.vt_lo, 0, (size_t)rows * E * 2, st));
     w.cap_rows = rows;
     w.cap_seqs = seqs;
+    w.gen++;
     return true;
 }
 
@@ -646,6 +660,11 @@ void drain_profile(Replica &R) {
         hipEventDestroy(p.second.second);
     }
     R.pending.clear();
+}
+
+void clear_graphs(Lane &ln) {
+    for (auto &g : ln.graphs) hipGraphExecDestroy(g.second);
+    ln.graphs.clear();
 }
 
 // Workspace hand-over between evals (Replica::ev_free): an eval's first
@@ -1180,6 +1199,7 @@ void free_replica(Replica &R) {
     drain_profile(R);
     for (auto &lp : R.lanes) {
         Lane &ln = *lp;
+        clear_graphs(ln);
         for (void *p : ln.ws.allocs) hipFree(p);
         if (ln.ws.h_tok) hipHostFree(ln.ws.h_tok);
         if (ln.ws.h_off) hipHostFree(ln.ws.h_off);
@@ -1230,9 +1250,9 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         ctx->fuse_min = value;
     } else if (k == "unfused") {
         ctx->unfused = value != 0;
-    } else if (k == "small_rows") {
+    } else if (k == "small_rows" || k == "graph_seqs") {
         if (need(value >= 0, "must be >= 0")) return -2;
-        ctx->small_rows = value;
+        (k == "small_rows" ? ctx->small_rows : ctx->graph_seqs) = value;
     } else if (k == "encode_lanes" || k == "encode_merge" || k == "encode_merge_rows") {
         if (need(value >= 1, "must be >= 1")) return -2;
         (k == "encode_lanes" ? ctx->encode_lanes : k == "encode_merge" ? ctx->encode_merge : ctx->encode_merge_rows) = value;
@@ -1240,6 +1260,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         set_err("bert_amd option: unknown option '%s'", k.c_str());
         return -2;
     }
+    ctx->opt_gen++;
     return 0;
 }
 
@@ -1250,7 +1271,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // fused kernel's weight grouping); every bert_amd_set_option key is accepted
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
-    static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows",
+    static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows", "graph_seqs",
                                  "encode_lanes", "encode_merge", "encode_merge_rows"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
@@ -1516,6 +1537,50 @@ bool grow_pinned(Workspace &w, int64_t rows, int64_t seqs, int64_t E) {
     return true;
 }
 
+// run_pipeline over the lane's workspace (tokens / offsets uploaded, h_off the
+// host offsets).  Small batches (<= graph_seqs sentences, fewer than fuse_min:
+// the unfused pair, so the pipeline makes no host copy; profiling off) replay a
+// HIP graph captured on the first batch of the same token offsets: the
+// launches' arguments depend only on the offsets, the workspace addresses
+// (graphs are dropped when it is reallocated) and the options (dropped on any
+// change).  At most 256 graphs per lane (then the cache starts over).
+bool run_host_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, int n, hipStream_t st) {
+    Workspace &w = ln.ws;
+    const int64_t M = w.h_off[n];
+    const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
+    if (R.prof || n > ctx->graph_seqs || n >= ctx->fuse_min || Mpad > w.cap_rows || n > w.cap_seqs)
+        return run_pipeline(ctx, R, ln, w.tok, w.off, w.h_off, n, w.out, st);
+    if (ln.graphs_ws_gen != w.gen || ln.graphs_opt_gen != ctx->opt_gen || ln.graphs.size() >= 256) {
+        clear_graphs(ln);
+        ln.graphs_ws_gen = w.gen;
+        ln.graphs_opt_gen = ctx->opt_gen;
+    }
+    std::vector<int32_t> key(w.h_off, w.h_off + n + 1);
+    auto it = ln.graphs.find(key);
+    if (it == ln.graphs.end()) {
+        HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        const bool ok = run_pipeline(ctx, R, ln, w.tok, w.off, w.h_off, n, w.out, st);
+        const std::string err = ok ? std::string() : g_err;
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(st, &g);
+        if (!ok || e != hipSuccess || !g) {
+            if (g) hipGraphDestroy(g);
+            set_err("graph capture: %s", ok ? hipGetErrorString(e) : err.c_str());
+            return false;
+        }
+        hipGraphExec_t ex = nullptr;
+        const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        if (ei != hipSuccess) {
+            set_err("graph instantiate: %s", hipGetErrorString(ei));
+            return false;
+        }
+        it = ln.graphs.emplace(std::move(key), ex).first;
+    }
+    HIP_OK(hipGraphLaunch(it->second, st));
+    return true;
+}
+
 // Evaluate sentences [s0, s1) of a host batch on replica R; results go
 // straight into the caller's embedding rows.
 bool eval_host_slice(bert_ctx *ctx, Replica &R, Lane &ln, bert_vocab_id **toks, const int32_t *ntok, float **embs, int s0,
@@ -1544,7 +1609,7 @@ bool eval_host_slice(bert_ctx *ctx, Replica &R, Lane &ln, bert_vocab_id **toks, 
     if (!ensure_workspace(ctx, ln, Mpad, n, st) || !ws_acquire(ln, st)) return false;
     HIP_OK(hipMemcpyAsync(w.tok, tok_direct ? toks[s0] : w.h_tok, (size_t)M * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(w.off, w.h_off, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
-    const bool ok = run_pipeline(ctx, R, ln, w.tok, w.off, w.h_off, n, w.out, st);
+    const bool ok = run_host_pipeline(ctx, R, ln, n, st);
     if (!ws_release(ln, st) || !ok) return false;
     const int E = ctx->hp.n_embd;
     // caller rows contiguous (one [n][E] array, the usual case): the embeddings
@@ -2203,7 +2268,7 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
     const std::string k = key;
     const std::pair<const char *, int32_t> opts[] = {
         {"split", ctx->split}, {"pack", ctx->pack}, {"fuse_min", ctx->fuse_min}, {"unfused", ctx->unfused},
-        {"small_rows", ctx->small_rows},
+        {"small_rows", ctx->small_rows}, {"graph_seqs", ctx->graph_seqs},
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},

@@ -825,6 +825,32 @@ def test_small_row_tiles_bitwise(shape, ftype, n_layer, opts, model_dir):
         m.close()
 
 
+def test_graph_replay_bitwise(model_dir):
+    """Host batches of <= graph_seqs sentences replay a HIP graph captured on
+    the first batch of the same token offsets: replays (new token ids, same
+    lengths), a workspace regrow between them (graphs dropped) and an option
+    change (dropped) all give the eager launches' embeddings bitwise."""
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    m = bertlib.BertModel(p)
+    try:
+        rng = np.random.default_rng(77)
+        mk = lambda n: [101] + rng.integers(1000, 30522, n - 2).tolist() + [102]
+        sets = [[mk(16)], [mk(16)], [mk(128)], [mk(7), mk(100)], [mk(7), mk(100)], [mk(300)], [mk(16)] * 3]
+        m.set_option("graph_seqs", 0)
+        want = [m.eval_batch(b) for b in sets]
+        m.set_option("graph_seqs", 8)
+        for rep in range(3):
+            for b, w in zip(sets, want):
+                assert np.array_equal(m.eval_batch(b), w), (rep, [len(t) for t in b])
+            if rep == 0:
+                m.eval_batch([mk(128)] * 64)  # regrows the workspace
+            if rep == 1:
+                m.set_option("small_rows", 0)
+        assert np.array_equal(m.eval(sets[0][0]), want[0][0])
+    finally:
+        m.close()
+
+
 def test_encode_batch_lanes_bitwise(model_dir):
     """bert_encode_batch with many small slices runs them on several lanes
     (workspaces + streams) at once; every embedding equals the one-batch
