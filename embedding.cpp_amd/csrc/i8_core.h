@@ -334,6 +334,8 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 16; i++) {
+            // (one v_fma_f32 per output: the packed v_pk_fma_f32 fold measured slower
+            // in every kernel, round 5 — DESIGN.md §3 "What bounds the GEMMs")
 #if I8_Q41_GENERIC
             float v;
             if constexpr (wt_q41(WT))
