@@ -808,7 +808,9 @@ def test_small_row_tiles_bitwise(shape, ftype, n_layer, opts, model_dir):
         lens = [1, 2, 5, 31, 32, 33, 64, 100, 127, 128, 129, 200, 512]
         toks = [[101] + rng.integers(1000, vocab, max(n - 2, 0)).tolist() + [102] for n in lens]
         toks[0] = [101]
-        batches = [[t] for t in toks] + [toks[1:9], [sentence(900 + i, 128, vocab) for i in range(16)]]
+        batches = [[t] for t in toks] + [toks[1:9], [sentence(900 + i, 128, vocab) for i in range(16)],
+                                         # >= 512 sentences: two row groups on two streams, each small
+                                         [[101, int(x), 102] for x in rng.integers(1000, vocab, 600)]]
         m.set_option("small_rows", 0)
         want = [m.eval_batch(b) for b in batches]
         m.set_option("small_rows", 4096)
