@@ -37,6 +37,9 @@ namespace bertamd {
 #ifndef I8_UP_T
 #define I8_UP_T 2
 #endif
+#ifndef I8_PRIO
+#define I8_PRIO 0  // A/B: static issue priority 1 for the later-dispatched half of the waves (FFN-up / FFN-down)
+#endif
 #ifndef I8_UP_AHEAD
 #define I8_UP_AHEAD 3  // weight blocks in flight (i8_core.h I8Pipe)
 #endif
@@ -56,6 +59,7 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ __attribute__((aligned(16))) uint16_t gtab[GELU_FLAT_LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+    if (I8_PRIO && wv >= NWV / 2) __builtin_amdgcn_s_setprio(1);
     const int nflat8 = (0x8000 + g.gelu.neg_n + 1 + 7) / 8;
     for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)g.gelu.full)[i];
     const float xlo = h2f((uint16_t)(0x8000 | g.gelu.neg_n));
@@ -151,6 +155,7 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
     const int ft0 = wv;
     const int col = 32 * ft0 + 16 * hh;
     if ((int)blockIdx.x >= n_mtiles) return;
+    if (I8_PRIO && wv >= 2 * NWV / 3) __builtin_amdgcn_s_setprio(1);  // (3 waves per SIMD: the youngest)
     int64_t m0n = (int64_t)xcd_linear(blockIdx.x, n_mtiles) * BM;
     I8Pipe<WT, NT, BM, F, I8_LN_AHEAD> pp;
     pp.prime(g, m0n, ft0);

@@ -123,6 +123,12 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
                         kernel (lower latency for small batches)
      "unfused" 0 | 1    1: every batch on the QKV GEMM + attention pair (A/B
                         checks; default 0)
+     "small_rows" n >= 0 batches of at most n padded rows (default 2048; one
+                        sentence is 128) run the int8 GEMMs in 32-row tiles
+                        (latency of small batches; 0 = never)
+     "graph_seqs" n >= 0 host batches of at most n sentences (and fewer than
+                        fuse_min) replay a captured HIP graph of their launches
+                        (default 0: measured no faster)
      "encode_lanes" n >= 1 bert_encode_batch: lanes per device, each a host
                         thread with its own workspace and streams (default 2;
                         BERT_AMD_ENCODE_LANES)
