@@ -1544,12 +1544,12 @@ bool grow_pinned(Workspace &w, int64_t rows, int64_t seqs, int64_t E) {
 // launches' arguments depend only on the offsets, the workspace addresses
 // (graphs are dropped when it is reallocated) and the options (dropped on any
 // change).  At most 256 graphs per lane (then the cache starts over).
-bool run_host_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, int n, hipStream_t st) {
+bool run_host_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, int n, hipStream_t st, const int32_t *d_out_row) {
     Workspace &w = ln.ws;
     const int64_t M = w.h_off[n];
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
-    if (R.prof || n > ctx->graph_seqs || n >= ctx->fuse_min || Mpad > w.cap_rows || n > w.cap_seqs)
-        return run_pipeline(ctx, R, ln, w.tok, w.off, w.h_off, n, w.out, st);
+    if (R.prof || d_out_row || n > ctx->graph_seqs || n >= ctx->fuse_min || Mpad > w.cap_rows || n > w.cap_seqs)
+        return run_pipeline(ctx, R, ln, w.tok, w.off, w.h_off, n, w.out, st, d_out_row);
     if (ln.graphs_ws_gen != w.gen || ln.graphs_opt_gen != ctx->opt_gen || ln.graphs.size() >= 256) {
         clear_graphs(ln);
         ln.graphs_ws_gen = w.gen;
@@ -1606,19 +1606,42 @@ bool eval_host_slice(bert_ctx *ctx, Replica &R, Lane &ln, bert_vocab_id **toks, 
         for (int s = s0; s < s1; s++) std::memcpy(w.h_tok + w.h_off[s - s0], toks[s], (size_t)ntok[s] * 4);
     const int64_t Mpad = std::max<int64_t>(GEMM_BM, (M + GEMM_BM - 1) / GEMM_BM * GEMM_BM);
     const hipStream_t st = ln.stream;
-    if (!ensure_workspace(ctx, ln, Mpad, n, st) || !ws_acquire(ln, st)) return false;
-    HIP_OK(hipMemcpyAsync(w.tok, tok_direct ? toks[s0] : w.h_tok, (size_t)M * 4, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(w.off, w.h_off, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
-    const bool ok = run_host_pipeline(ctx, R, ln, n, st);
-    if (!ws_release(ln, st) || !ok) return false;
     const int E = ctx->hp.n_embd;
     // caller rows contiguous (one [n][E] array, the usual case): the embeddings
     // go straight from the device into them, without the pinned bounce buffer
-    // and the host copy (host-API batch 1024 x 128, tools/host_ab.sh: minimum 6.80-6.85 -> 6.71-6.78 ms)
+    // and the host copy (host-API batch 1024 x 128, tools/host_ab.sh: minimum 6.80-6.85 -> 6.71-6.78 ms).
+    // Rows that are a permutation of one [n][E] block (bert_encode_batch's
+    // length-sorted inputs, eval_grouped's tile order): the pool kernel writes
+    // each sentence into its caller row of w.out (d_out_row) and one copy lands
+    // them all in place.
     bool direct = true;
     for (int s = s0 + 1; direct && s < s1; s++) direct = embs[s] == embs[s0] + (size_t)(s - s0) * E;
-    if (direct) {
-        HIP_OK(hipMemcpyAsync(embs[s0], w.out, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
+    float *base = embs[s0];
+    std::vector<int32_t> out_row;
+    if (!direct) {
+        for (int s = s0 + 1; s < s1; s++) base = std::min(base, embs[s]);
+        out_row.resize(n);
+        std::vector<char> seen(n, 0);
+        bool perm = true;
+        for (int s = s0; perm && s < s1; s++) {
+            const size_t d = (size_t)(embs[s] - base);
+            perm = d % E == 0 && d / E < (size_t)n && !seen[d / E];
+            if (perm) {
+                seen[d / E] = 1;
+                out_row[s - s0] = (int32_t)(d / E);
+            }
+        }
+        if (!perm) out_row.clear();
+    }
+    if (!ensure_workspace(ctx, ln, Mpad, n, st) || !ws_acquire(ln, st)) return false;
+    HIP_OK(hipMemcpyAsync(w.tok, tok_direct ? toks[s0] : w.h_tok, (size_t)M * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(w.off, w.h_off, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
+    // (pageable source: staged before the call returns)
+    if (!out_row.empty()) HIP_OK(hipMemcpyAsync(w.perm, out_row.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    const bool ok = run_host_pipeline(ctx, R, ln, n, st, out_row.empty() ? nullptr : w.perm);
+    if (!ws_release(ln, st) || !ok) return false;
+    if (direct || !out_row.empty()) {
+        HIP_OK(hipMemcpyAsync(direct ? embs[s0] : base, w.out, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         drain_profile(R);
         return true;
@@ -1957,28 +1980,36 @@ void bert_encode_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, i
     // makes each slice's lengths similar, so padding and tile waste stay small.
     if (!ctx || n_inputs <= 0 || !texts || !embeddings) return;
     const int32_t N = ctx->hp.n_max_tokens;
-    std::vector<bert_vocab_id> buf((size_t)N * n_inputs);
     std::vector<int32_t> ntok(n_inputs);
     std::vector<bert_vocab_id *> ptr(n_inputs);
     // tokenisation on n_threads host threads (the reference's thread count;
     // its CPU graph used them, bert.cpp:1128): contiguous ranges of inputs,
-    // each into its own N-token slots of `buf` (the tokenizer is stateless)
+    // each thread appending its sentences' ids to its own array (the tokenizer
+    // is stateless; no n_inputs x n_max_tokens buffer to zero and fault in)
     const int nt = std::max(1, std::min({(int)n_threads, n_inputs / 64 + 1,
                                          (int)std::max(1u, std::thread::hardware_concurrency())}));
-    auto tok_range = [&](int a, int b) {
+    std::vector<std::vector<bert_vocab_id>> part(nt);
+    std::vector<size_t> at(n_inputs);
+    auto tok_range = [&](int t, int a, int b) {
+        std::vector<bert_vocab_id> one((size_t)N);
+        std::vector<bert_vocab_id> &v = part[t];
+        v.reserve((size_t)(b - a) * 48);
         for (int i = a; i < b; i++) {
-            ptr[i] = buf.data() + (size_t)i * N;
-            bert_tokenize(ctx, texts[i], ptr[i], &ntok[i], N);
+            bert_tokenize(ctx, texts[i], one.data(), &ntok[i], N);
+            at[i] = v.size();
+            v.insert(v.end(), one.begin(), one.begin() + std::max(0, ntok[i]));
         }
     };
+    auto lo = [&](int t) { return (int)((int64_t)n_inputs * t / nt); };
     if (nt == 1) {
-        tok_range(0, n_inputs);
+        tok_range(0, 0, n_inputs);
     } else {
         std::vector<std::thread> th;
-        for (int t = 0; t < nt; t++)
-            th.emplace_back(tok_range, (int)((int64_t)n_inputs * t / nt), (int)((int64_t)n_inputs * (t + 1) / nt));
+        for (int t = 0; t < nt; t++) th.emplace_back(tok_range, t, lo(t), lo(t + 1));
         for (auto &t : th) t.join();
     }
+    for (int t = 0; t < nt; t++)  // (the arrays no longer grow)
+        for (int i = lo(t); i < lo(t + 1); i++) ptr[i] = part[t].data() + at[i];
     std::vector<int> idx(n_inputs);
     for (int i = 0; i < n_inputs; i++) idx[i] = i;
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return ntok[a] < ntok[b]; });
