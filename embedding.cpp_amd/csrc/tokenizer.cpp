@@ -13,6 +13,12 @@ namespace {
 
 #include "unicode_tables.inc"
 
+// FNV-1a over bytes, continuing from h (the vocabulary table's hash)
+inline uint32_t fnv1a(uint32_t h, const char *p, size_t n) {
+    for (size_t i = 0; i < n; i++) h = (h ^ (uint8_t)p[i]) * 16777619u;
+    return h;
+}
+
 template <size_t N>
 bool in_ranges(const uint32_t (&r)[N][2], uint32_t cp) {
     size_t lo = 0, hi = N;
@@ -263,6 +269,24 @@ bool WordPieceTokenizer::load(const std::string &json, std::string &err) {
     std::sort(added_.begin(), added_.end(), [](auto &a, auto &b) { return a.first.size() > b.first.size(); });
     if (!vocab_.count(unk_)) { err = "tokenizer.json: unk token not in vocab"; return false; }
     unk_id_ = vocab_.at(unk_);
+    {
+        size_t cap = 16;
+        while (cap < 2 * vocab_.size()) cap *= 2;
+        vslots_.assign(cap, VSlot{});
+        vmask_ = (uint32_t)(cap - 1);
+        varena_.clear();
+        for (auto &kv : vocab_) {
+            VSlot e;
+            e.hash = fnv1a(2166136261u, kv.first.data(), kv.first.size());
+            e.off = (uint32_t)varena_.size();
+            e.len = (uint32_t)kv.first.size();
+            e.id = kv.second;
+            varena_ += kv.first;
+            uint32_t i = e.hash & vmask_;
+            while (vslots_[i].id >= 0) i = (i + 1) & vmask_;
+            vslots_[i] = e;
+        }
+    }
     for (auto &a : added_) added_first_[(unsigned char)a.first[0]] = true;
     // the ASCII fast path's tables, from the same predicates normalize() and
     // pre_tokenize() apply (NFD and accent stripping are the identity on ASCII)
@@ -281,11 +305,25 @@ bool WordPieceTokenizer::load(const std::string &json, std::string &err) {
     return true;
 }
 
+int32_t WordPieceTokenizer::lookup(const char *p, size_t n, bool cont) const {
+    const size_t pl = cont ? prefix_.size() : 0;
+    uint32_t h = 2166136261u;
+    if (cont) h = fnv1a(h, prefix_.data(), pl);
+    h = fnv1a(h, p, n);
+    for (uint32_t i = h & vmask_;; i = (i + 1) & vmask_) {
+        const VSlot &e = vslots_[i];
+        if (e.id < 0) return -1;
+        if (e.hash == h && e.len == pl + n && std::memcmp(varena_.data() + e.off, prefix_.data(), pl) == 0 &&
+            std::memcmp(varena_.data() + e.off + pl, p, n) == 0)
+            return e.id;
+    }
+}
+
 // WordPiece on one pre-token w of nchars characters (byte offset of char k:
 // off[k]): greedy longest match from the left, "##" continuations, [UNK] for
-// the whole word if any piece is missing.  `buf` is scratch.
-void WordPieceTokenizer::wordpiece(const std::string &w, size_t nchars, const size_t *off, std::vector<int32_t> &ids,
-                                   std::string &buf) const {
+// the whole word if any piece is missing.
+void WordPieceTokenizer::wordpiece(const std::string &w, size_t nchars, const size_t *off,
+                                   std::vector<int32_t> &ids) const {
     if ((int)nchars > max_chars_) { ids.push_back(unk_id_); return; }
     const size_t base = ids.size();
     size_t start = 0;
@@ -293,11 +331,8 @@ void WordPieceTokenizer::wordpiece(const std::string &w, size_t nchars, const si
         size_t end = nchars;
         int32_t found = -1;
         while (start < end) {
-            buf.clear();
-            if (start > 0) buf += prefix_;
-            buf.append(w, off[start], off[end] - off[start]);
-            auto it = vocab_.find(buf);
-            if (it != vocab_.end()) { found = it->second; break; }
+            found = lookup(w.data() + off[start], off[end] - off[start], start > 0);
+            if (found >= 0) break;
             end--;
         }
         if (found < 0) {
@@ -390,7 +425,7 @@ std::vector<int32_t> WordPieceTokenizer::encode(const std::string &text) const {
         }
         if (start < text.size()) pieces.emplace_back(text.substr(start), -1);
     }
-    std::string buf, word;
+    std::string word;
     std::vector<size_t> aoff;
     for (auto &pc : pieces) {
         if (pc.second >= 0) { ids.push_back(pc.second); continue; }
@@ -403,7 +438,7 @@ std::vector<int32_t> WordPieceTokenizer::encode(const std::string &text) const {
                     aoff.resize(word.size() + 1);
                     for (size_t k = 0; k < aoff.size(); k++) aoff[k] = k;
                 }
-                wordpiece(word, word.size(), aoff.data(), ids, buf);
+                wordpiece(word, word.size(), aoff.data(), ids);
                 word.clear();
             };
             for (char ch : t) {
@@ -443,10 +478,8 @@ std::vector<int32_t> WordPieceTokenizer::encode(const std::string &text) const {
                 size_t end = chars.size();
                 int32_t found = -1;
                 while (start < end) {
-                    std::string s = w.substr(off[start], off[end] - off[start]);
-                    if (start > 0) s = prefix_ + s;
-                    auto it = vocab_.find(s);
-                    if (it != vocab_.end()) { found = it->second; break; }
+                    found = lookup(w.data() + off[start], off[end] - off[start], start > 0);
+                    if (found >= 0) break;
                     end--;
                 }
                 if (found < 0) { bad = true; break; }

@@ -45,8 +45,18 @@ private:
     // at load): 0 drop, 1 whitespace, 2 punctuation, 3 word character; and the
     // byte after normalisation
     uint8_t ascii_class_[128] = {}, ascii_norm_[128] = {};
-    void wordpiece(const std::string &w, size_t nchars, const size_t *off, std::vector<int32_t> &ids,
-                   std::string &buf) const;
+    // the vocabulary again as an open-addressing table over one byte arena, so
+    // that WordPiece looks candidate pieces up without building a string each
+    struct VSlot {
+        uint32_t hash = 0, off = 0, len = 0;
+        int32_t id = -1;
+    };
+    std::string varena_;
+    std::vector<VSlot> vslots_;
+    uint32_t vmask_ = 0;
+    // id of prefix_ + [p, p + n) (cont) or of [p, p + n), -1 if absent
+    int32_t lookup(const char *p, size_t n, bool cont) const;
+    void wordpiece(const std::string &w, size_t nchars, const size_t *off, std::vector<int32_t> &ids) const;
 };
 
 }  // namespace bertamd
