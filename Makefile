@@ -15,7 +15,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wn
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
 HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
 
-all: $(BUILD)/libbert.so $(BUILD)/div_check $(BUILD)/qkva_check $(BUILD)/mfma_bf16_split_probe
+all: $(BUILD)/libbert.so $(BUILD)/div_check $(BUILD)/qkva_check $(BUILD)/mfma_bf16_split_probe $(BUILD)/tok_bench
 
 $(BUILD)/obj/%.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/bert.h include/bert_amd.h
 	@mkdir -p $(dir $@)
@@ -54,6 +54,11 @@ $(BUILD)/div_check: tools/div_check.hip
 $(BUILD)/mfma_bf16_split_probe: tools/mfma_bf16_split_probe.hip
 	@mkdir -p $(BUILD)
 	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@
+
+# host-only tokenizer timing (development; DESIGN.md §6 consumer line)
+$(BUILD)/tok_bench: tools/tok_bench.cpp $(BUILD)/obj/gguf_io.o $(BUILD)/obj/tokenizer.o
+	@mkdir -p $(BUILD)
+	$(CXX) -O2 -std=c++17 -I$(SRC) $^ -o $@ -lpthread
 
 # development timing harness for the int8-MFMA GEMMs (not shipped)
 
