@@ -506,6 +506,41 @@ def test_encode_batch_slices_sorted_and_bounded(model_dir):
         m.close()
 
 
+def test_output_rows_any_layout(model_dir):
+    """The embedding rows a caller passes: one contiguous array (one copy back),
+    a permutation of one array's rows (the pool kernel writes each sentence into
+    its row, runtime.cpp eval_host_slice), separate arrays and one array with a
+    row stride (the pinned bounce + host scatter) — bitwise the same, through
+    bert_eval_batch and bert_encode_batch."""
+    import ctypes
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    rng = np.random.default_rng(31)
+    toks = [[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in rng.integers(3, 129, 37)]
+    want = m.eval_batch(toks)
+    n, E = len(toks), want.shape[1]
+    I_P = ctypes.POINTER(ctypes.c_int32)
+    arrs = [np.ascontiguousarray(t, np.int32) for t in toks]
+    tp = (I_P * n)(*[a.ctypes.data_as(I_P) for a in arrs])
+    tn = (ctypes.c_int32 * n)(*[len(a) for a in arrs])
+    perm = rng.permutation(n)
+    block = np.zeros((n, E), np.float32)          # a permutation of one array's rows
+    sep = [np.zeros(E, np.float32) for _ in range(n)]  # separate arrays
+    strided = np.zeros((n, 2 * E), np.float32)    # rows with a stride: not one [n][E] block
+    for rows, get in ((lambda i: block[perm[i]], lambda: block[perm]),
+                      (lambda i: sep[i], lambda: np.stack(sep)),
+                      (lambda i: strided[i, :E], lambda: strided[:, :E])):
+        ep = (bertlib.F_P * n)(*[rows(i).ctypes.data_as(bertlib.F_P) for i in range(n)])
+        m.lib.bert_eval_batch(m.ctx, 1, n, tp, tn, ep)
+        assert np.array_equal(get(), want)
+    texts = [" ".join(f"w{int(x)}" for x in rng.integers(0, 500, int(k))) for k in rng.integers(1, 60, 50)]
+    enc = m.encode(texts, batch_size=0)
+    sep2 = [np.zeros(E, np.float32) for _ in texts]
+    c_texts = (ctypes.c_char_p * len(texts))(*[t.encode() for t in texts])
+    ep = (bertlib.F_P * len(texts))(*[a.ctypes.data_as(bertlib.F_P) for a in sep2])
+    m.lib.bert_encode_batch(m.ctx, 1, len(texts), len(texts), c_texts, ep)
+    assert np.array_equal(np.stack(sep2), enc)
+
+
 def test_mixed_lengths_group_like_separate_batches(model_dir):
     """A host batch mixing <=128 and >128-token sentences runs as two ragged
     batches (fused QKV+attention for the short ones); each result equals the
