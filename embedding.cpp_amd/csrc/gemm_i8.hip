@@ -438,6 +438,77 @@ __global__ __launch_bounds__(768) void i8_qkv_kernel(GemmArgs g, int n_mtiles, i
 // (A 12-wave form with the LayerNorm in its epilogue — whole rows per
 // workgroup, 4 workgroups for one sentence — measured 24 us against 20 us for
 // the two kernels: at 4 CUs the block steps are issue-bound.)
+// Epilogue of a 32 x 32 small tile in the MFMA output layout: token `row`,
+// this lane's 16 outputs (f-tile ft0, lane half hh).
+// Its global operands (bias; EPI_RESID: the residual x) are loaded by
+// i8_small_epi_pre, which a kernel may issue before its main loop.
+struct I8EpiPre {
+    float4v b[4], x[4];
+};
+template <int EPI>
+__device__ __forceinline__ void i8_small_epi_pre(const GemmArgs &g, int64_t row, int ft0, int hh, I8EpiPre &pre) {
+    const int f0 = 32 * ft0 + 16 * hh;
+#pragma unroll
+    for (int q = 0; q < 4; q++) pre.b[q] = *(const float4v *)(g.bias + f0 + 4 * q);
+    if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) pre.x[q] = *(const float4v *)(g.X + row * g.N + f0 + 4 * q);
+    }
+}
+template <int WT, int EPI>
+__device__ __forceinline__ void i8_small_epi(const GemmArgs &g, const float16v &acc, int64_t row, int ft0, int hh,
+                                             const I8EpiPre &pre) {
+    const int f0 = 32 * ft0 + 16 * hh;
+    float bias[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) bias[4 * q + j] = pre.b[q][j];
+    if constexpr (EPI == EPI_QKV) {  // i8_qkv_kernel's epilogue
+        const int E = g.N / 3, D = g.head_dim;
+        const int hd = f0 / (3 * D), part = (f0 - hd * 3 * D) / D, dd = f0 - hd * 3 * D - part * D;
+        half8 hv[2], lv[2];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const float y = bias[i] + acc[i];
+            const _Float16 yh = (_Float16)y;
+            hv[i >> 3][i & 7] = yh;
+            lv[i >> 3][i & 7] = (_Float16)(y - (float)yh);
+        }
+        if (part < 2) {
+            const int64_t o = row * (2 * E) + part * E + hd * D + dd;
+            *(half8 *)(g.qk_hi + o) = hv[0];
+            *(half8 *)(g.qk_hi + o + 8) = hv[1];
+            *(half8 *)(g.qk_lo + o) = lv[0];
+            *(half8 *)(g.qk_lo + o + 8) = lv[1];
+        } else {
+            const int64_t c0 = hd * D + dd;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                ((_Float16 *)g.vt_hi)[(c0 + i) * g.ldv + row] = hv[i >> 3][i & 7];
+                ((_Float16 *)g.vt_lo)[(c0 + i) * g.ldv + row] = lv[i >> 3][i & 7];
+            }
+        }
+    } else if constexpr (EPI == EPI_GELU_ACT) {  // i8_up_gelu_kernel's epilogue
+        const uint16_t *gt = g.gelu.full;
+        const float xlo = h2f((uint16_t)(0x8000 | g.gelu.neg_n));
+        float y[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) y[i] = h2f(gt[f2h(fmaxf(bias[i] + acc[i], xlo))]);
+        i8_store_q8_half<WT>(g.out_act, g.N, row, ft0, hh, y);
+    } else {  // EPI_RESID: i8_resid_kernel's / i8_ln384_kernel's v = (b + W.x) + x
+        float4v *xp = (float4v *)(g.X + row * g.N + f0);
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const float4v x4 = pre.x[qq];
+            float4v o;
+#pragma unroll
+            for (int j = 0; j < 4; j++) o[j] = (bias[4 * qq + j] + acc[4 * qq + j]) + x4[j];
+            xp[qq] = o;
+        }
+    }
+}
+
 #ifndef I8_SK_WAVES
 #define I8_SK_WAVES 2
 #endif
@@ -546,58 +617,102 @@ __global__ __launch_bounds__(NW * 64) void i8_small_kernel(GemmArgs g, int n_mti
         }
         __syncthreads();
     }
-    const int64_t row = m0 + l32;
-    const int f0 = 32 * ft0 + 16 * hh;
-    float bias[16];
+    I8EpiPre pre;
+    i8_small_epi_pre<EPI>(g, m0 + l32, ft0, hh, pre);
+    i8_small_epi<WT, EPI>(g, acc[0][0], m0 + l32, ft0, hh, pre);
+}
+
+// Small batches, Q4_0: the K loop split over the waves of a workgroup.  One
+// 32-token x 32-feature tile per workgroup; wave w computes blocks
+// b = NW r + w (r < R rounds; every operand of its blocks loaded up front) —
+// isum on the int8 MFMA and d_w * d_a on the fp16 MFMA exactly as i8_block —
+// and leaves float(isum) and d_w d_a in LDS; then each thread folds its
+// outputs over the round's blocks in block order, acc = fma(float(isum),
+// d_w d_a, acc), the batch kernels' chain bit for bit.  The per-block products
+// are independent, only the fold is sequential, so the chain (NW fmas a round
+// per output) is all that is serial.  Epilogue: i8_small_epi in wave 0.
+#ifndef I8_KS
+#define I8_KS 1
+#endif
+#ifndef I8_KS_NW48  // waves for K <= 1536 (48 / I8_KS_NW48 rounds)
+#define I8_KS_NW48 16
+#endif
+
+template <int EPI, int NW, int R>
+__global__ __launch_bounds__(NW * 64) void i8_small_ks_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
+    constexpr int NT = NW * 64, PER = (1024 + NT - 1) / NT;
+    __shared__ float fis[NW][1024], fdd[NW][1024];  // [wave][i 64 + lane]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+    const int nwg = n_mtiles * n_ntiles;
+    if ((int)blockIdx.x >= nwg) return;
+    const int lin = xcd_linear(blockIdx.x, nwg);
+    const int mt = lin / n_ntiles, ft0 = lin - mt * n_ntiles;
+    const int64_t row = (int64_t)mt * 32 + l32;
+    const int K = g.K, nkb = K >> 5, nr = (nkb + NW - 1) / NW;
+
+    int4v wq[R], xa[R];
+    uint32_t dw[R], da[R];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
+    for (int r = 0; r < R; r++) {
+        const int b = min(NW * r + wv, nkb - 1);  // clamped: a wave past the last block loads and drops it
+        wq[r] = i8_wq(g.Wi, nkb, ft0, b);
+        xa[r] = *(const int4v *)((const int8_t *)g.A.q + row * K + 32 * b + 16 * hh);
+        dw[r] = ((const uint16_t *)g.Wi.dh)[(((int64_t)ft0 * (nkb >> 2) + (b >> 2)) * 32 + l32) * 4 + (b & 3)];
+        da[r] = ((const uint16_t *)g.A.d)[row * nkb + b];
     }
-    if constexpr (EPI == EPI_QKV) {  // i8_qkv_kernel's epilogue
-        const int E = g.N / 3, D = g.head_dim;
-        const int hd = f0 / (3 * D), part = (f0 - hd * 3 * D) / D, dd = f0 - hd * 3 * D - part * D;
-        half8 hv[2], lv[2];
+    I8EpiPre pre;  // the epilogue's global operands, issued with the block operands (wave 0's)
+    if (wv == 0) i8_small_epi_pre<EPI>(g, row, ft0, hh, pre);
+    const float16v zf = {};
+    float acc[PER];
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const float y = bias[i] + acc[0][0][i];
-            const _Float16 yh = (_Float16)y;
-            hv[i >> 3][i & 7] = yh;
-            lv[i >> 3][i & 7] = (_Float16)(y - (float)yh);
-        }
-        if (part < 2) {
-            const int64_t o = row * (2 * E) + part * E + hd * D + dd;
-            *(half8 *)(g.qk_hi + o) = hv[0];
-            *(half8 *)(g.qk_hi + o + 8) = hv[1];
-            *(half8 *)(g.qk_lo + o) = lv[0];
-            *(half8 *)(g.qk_lo + o + 8) = lv[1];
-        } else {
-            const int64_t c0 = hd * D + dd;
+    for (int p = 0; p < PER; p++) acc[p] = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        if (r >= nr) break;
+        if (NW * r + wv < nkb) {
+            const int16v is = __builtin_amdgcn_mfma_i32_32x32x32_i8(wq[r], xa[r], __builtin_bit_cast(int16v, zf), 0, 0, 0);
+            const int4v ws = int4v{(int)dw[r], 0, 0, 0}, oh = int4v{hh ? 0 : (int)da[r], 0, 0, 0};
+            const float16v dd = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ws),
+                                                                        __builtin_bit_cast(half8, oh), zf, 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 16; i++) {
-                ((_Float16 *)g.vt_hi)[(c0 + i) * g.ldv + row] = hv[i >> 3][i & 7];
-                ((_Float16 *)g.vt_lo)[(c0 + i) * g.ldv + row] = lv[i >> 3][i & 7];
+                fis[wv][i * 64 + lane] = (float)is[i];
+                fdd[wv][i * 64 + lane] = dd[i];
             }
         }
-    } else if constexpr (EPI == EPI_GELU_ACT) {  // i8_up_gelu_kernel's epilogue
-        const uint16_t *gt = g.gelu.full;
-        const float xlo = h2f((uint16_t)(0x8000 | g.gelu.neg_n));
-        float y[16];
+        __syncthreads();
+        const int nb = min(NW, nkb - NW * r);
 #pragma unroll
-        for (int i = 0; i < 16; i++) y[i] = h2f(gt[f2h(fmaxf(bias[i] + acc[0][0][i], xlo))]);
-        i8_store_q8_half<WT>(g.out_act, g.N, row, ft0, hh, y);
-    } else {  // EPI_RESID: i8_resid_kernel's / i8_ln384_kernel's v = (b + W.x) + x
-        float4v *xp = (float4v *)(g.X + row * g.N + f0);
+        for (int p = 0; p < PER; p++) {
+            const int e = tid + p * NT;
+            if (1024 % NT == 0 || e < 1024) {
+                if (nb == NW) {  // a whole round: every LDS read issued before the chain
+                    float fi[NW], fd[NW];
 #pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const float4v x4 = xp[qq];
-            float4v o;
+                    for (int w = 0; w < NW; w++) {
+                        fi[w] = fis[w][e];
+                        fd[w] = fdd[w][e];
+                    }
 #pragma unroll
-            for (int j = 0; j < 4; j++) o[j] = (bias[4 * qq + j] + acc[0][0][4 * qq + j]) + x4[j];
-            xp[qq] = o;
+                    for (int w = 0; w < NW; w++) acc[p] = __builtin_fmaf(fi[w], fd[w], acc[p]);
+                } else {
+                    for (int w = 0; w < nb; w++) acc[p] = __builtin_fmaf(fis[w][e], fdd[w][e], acc[p]);
+                }
+            }
         }
+        __syncthreads();
     }
+#pragma unroll
+    for (int p = 0; p < PER; p++) {
+        const int e = tid + p * NT;
+        if (1024 % NT == 0 || e < 1024) fis[0][e] = acc[p];
+    }
+    __syncthreads();
+    if (wv) return;
+    float16v a;
+#pragma unroll
+    for (int i = 0; i < 16; i++) a[i] = fis[0][i * 64 + lane];
+    i8_small_epi<W_Q4_0, EPI>(g, a, row, ft0, hh, pre);
 }
 
 // LayerNorm of 384-wide rows after i8_small_kernel's residual: i8_ln384_kernel's
@@ -613,6 +728,12 @@ __global__ __launch_bounds__(256) void i8_ln384_rows_kernel(GemmArgs g, int Mpad
     const bool on = w < 12;
     const int col = 32 * (on ? w : 0) + 16 * hh;
     float *xr = g.X + row * 384 + col;
+    float4v lw[4], lb[4];  // issued with the row's loads, not after the reductions' barriers
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) {
+        lw[qq] = *(const float4v *)(g.ln_w + col + 4 * qq);
+        lb[qq] = *(const float4v *)(g.ln_b + col + 4 * qq);
+    }
     float v[16];
 #pragma unroll
     for (int qq = 0; qq < 4; qq++) {
@@ -620,31 +741,36 @@ __global__ __launch_bounds__(256) void i8_ln384_rows_kernel(GemmArgs g, int Mpad
 #pragma unroll
         for (int j = 0; j < 4; j++) v[4 * qq + j] = x4[j];
     }
-    auto row_sum = [&](double s) {  // s: this lane's 16-term sum; the row total in every lane
+    // the twelve lane sums pass through LDS (twelve independent reads; a chain
+    // of twelve shuffles measured 2 us of this kernel's 4.5), summed in order
+    __shared__ double part[2][4][12];
+    const int wv = threadIdx.x >> 6;
+    auto row_sum = [&](double s, int j) {  // s: this lane's 16-term sum; the row total in every lane
         s += __shfl_xor(s, 32);
+        if (lane < 12) part[j][wv][lane] = s;
+        __syncthreads();
         double tot = 0.0;
 #pragma unroll
-        for (int k = 0; k < 12; k++) tot += __shfl(s, k);
+        for (int k = 0; k < 12; k++) tot += part[j][wv][k];
         return tot;
     };
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; i++) s += (double)v[i];
-    const float mean = (float)(row_sum(s) / 384);
+    const float mean = (float)(row_sum(s, 0) / 384);
     double s2 = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; i++) {
         v[i] = v[i] - mean;
         s2 += (double)(v[i] * v[i]);
     }
-    const float var = (float)(row_sum(s2) / 384);
+    const float var = (float)(row_sum(s2, 1) / 384);
     const float scale = 1.0f / sqrtf(var + g.eps);
     if (!on) return;  // both lane halves of a column block leave together (i8_store_q8_half pairs them)
     float y[16];
 #pragma unroll
     for (int qq = 0; qq < 4; qq++) {
-        const float4v w4 = *(const float4v *)(g.ln_w + col + 4 * qq);
-        const float4v b4 = *(const float4v *)(g.ln_b + col + 4 * qq);
+        const float4v w4 = lw[qq], b4 = lb[qq];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             float z = v[4 * qq + j] * scale;
@@ -720,6 +846,32 @@ static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s
     if (a.N % (32 * NW) || (epi == EPI_LN && a.N != 384)) return hipErrorInvalidValue;
     const int nt = a.N / (32 * NW);
     const dim3 grid(mt * nt), block(NW * 64);
+    if constexpr (WT == W_Q4_0) {
+        const int nkb = a.K >> 5;
+        if (I8_KS && nkb <= 96 && (epi != EPI_QKV || (a.head_dim > 0 && a.head_dim % 16 == 0 && (a.N / 3) % a.head_dim == 0))) {
+            const dim3 gk(mt * (a.N / 32));
+            const int ntk = a.N / 32;
+            auto go = [&](auto kern, int nw) { hipLaunchKernelGGL(kern, gk, dim3(nw * 64), 0, s, a, mt, ntk); };
+            const int e2 = epi == EPI_LN ? EPI_RESID : epi;
+#define I8_KS_GO(E)                                                                       \
+    (nkb <= 12 ? go(i8_small_ks_kernel<E, 12, 1>, 12)                                  \
+               : nkb <= 48 ? go(i8_small_ks_kernel<E, I8_KS_NW48, 48 / I8_KS_NW48>, I8_KS_NW48)             \
+                           : go(i8_small_ks_kernel<E, 16, 6>, 16))
+            switch (e2) {
+                case EPI_QKV: I8_KS_GO(EPI_QKV); break;
+                case EPI_GELU_ACT: I8_KS_GO(EPI_GELU_ACT); break;
+                case EPI_RESID: I8_KS_GO(EPI_RESID); break;
+                default: return hipErrorInvalidValue;
+            }
+#undef I8_KS_GO
+            if (epi == EPI_LN) {
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL((i8_ln384_rows_kernel<WT>), dim3(Mpad / 4), dim3(256), 0, s, a, Mpad);
+            }
+            return hipGetLastError();
+        }
+    }
     switch (epi) {
         case EPI_QKV:
             if (a.head_dim <= 0 || a.head_dim % 16 || (a.N / 3) % a.head_dim) return hipErrorInvalidValue;

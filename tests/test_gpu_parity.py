@@ -827,11 +827,14 @@ def test_small_batches_unfused_bitwise_fused(shape, ftype, model_dir):
     ("minilm", "q4_1", None, {"i8": "all"}),
     ("minilm", "q4_1", None, {"i8": "all", "q41bf": 1}),
     ("bge-large", "q4_1", 2, {"i8": "all"}),
+    ("e5-base", "q4_0", 2, {"i8": "all"}),  # K = 768 / 3072: the K-split kernel's 2- and 6-round forms
 ])
 def test_small_row_tiles_bitwise(shape, ftype, n_layer, opts, model_dir):
     """Batches of at most small_rows padded rows (one server sentence: 128) run
-    the int8 GEMMs in 32-row tiles (gemm_i8.hip i8_small_kernel, and for
-    n_embd 384 the LayerNorm in i8_ln384_kernel's reduction order) and the
+    the int8 GEMMs in 32-row tiles (gemm_i8.hip i8_small_kernel; Q4_0 with
+    K <= 3072: i8_small_ks_kernel, the K loop split over waves, the fold in
+    block order; for n_embd 384 the LayerNorm in i8_ln384_kernel's reduction
+    order) and the
     split-fp16 LayerNorm GEMM in 32-row tiles: every embedding bitwise the
     batch kernels' (small_rows 0), alone or in a batch, so a sentence's result
     does not depend on the batch it came in."""

@@ -24,6 +24,7 @@ ap.add_argument("--runs", type=int, default=200)
 ap.add_argument("--model-dir", default=os.environ.get("BERT_AMD_MODEL_DIR", "/tmp/bert_amd_models"))
 ap.add_argument("--configs", default="0:0,2048:0,2048:8,0:8", help="small_rows:graph_seqs pairs")
 ap.add_argument("--lengths", default="16,128")
+ap.add_argument("--opts", default="", help="extra options, k=v[,k=v]")
 args = ap.parse_args()
 
 os.makedirs(args.model_dir, exist_ok=True)
@@ -33,13 +34,16 @@ if not os.path.exists(path):
     bertlib.synth_model(tmp, args.shape, args.ftype, seed=20250117, w_std=0.05)
     os.replace(tmp, path)
 m = bertlib.BertModel(path, devices=[0])
+for kv in filter(None, args.opts.split(",")):
+    k, v = kv.split("=")
+    m.set_option(k, int(v))
 rng = np.random.default_rng(7)
 ref = {}
 for cfg in args.configs.split(","):
     sr, gs = (int(x) for x in cfg.split(":"))
     m.set_option("small_rows", sr)
     m.set_option("graph_seqs", gs)
-    res = {"small_rows": sr, "graph_seqs": gs}
+    res = {"small_rows": sr, "graph_seqs": gs, "opts": args.opts}
     for n in (int(x) for x in args.lengths.split(",")):
         toks = [101] + rng.integers(1000, 30000, n - 2).tolist() + [102]
         for _ in range(20):
