@@ -835,7 +835,7 @@ def test_small_row_tiles_bitwise(shape, ftype, n_layer, opts, model_dir):
     K <= 3072: i8_small_ks_kernel, the K loop split over waves, the fold in
     block order; for n_embd 384 the LayerNorm in i8_ln384_kernel's reduction
     order) and the
-    split-fp16 LayerNorm GEMM in 32-row tiles: every embedding bitwise the
+    split-fp16 LayerNorm GEMM in 16-row tiles: every embedding bitwise the
     batch kernels' (small_rows 0), alone or in a batch, so a sentence's result
     does not depend on the batch it came in."""
     p = ensure_model(model_dir, shape, ftype, 0.05, n_layer)
@@ -857,6 +857,11 @@ def test_small_row_tiles_bitwise(shape, ftype, n_layer, opts, model_dir):
             bad = [i for i in range(len(b)) if not np.array_equal(got[i], w[i])]
             assert not bad, (opts, [len(b[i]) for i in bad])
         assert np.array_equal(m.eval(toks[9]), want[9][0])
+        # sentences of the 16 x 128 batch (batch kernels) alone: the small forms,
+        # O + LN included (<= 512 rows: 16-row tiles)
+        b16, w16 = batches[len(toks) + 1], want[len(toks) + 1]
+        for i in (0, 7, 15):
+            assert np.array_equal(m.eval_batch([b16[i]])[0], w16[i]), (opts, i)
         if ftype == "q4_0":  # (Q4_1: the golden fixtures, with ggml's order-spread bounds)
             import oracle
             c = cos(np.concatenate(want[:4]), oracle.Oracle(p).eval_batch(toks[:4], 0))

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 REPS=$1; shift
 timeout -k 10 400 python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
-  -k "small_row_tiles or graph_replay or output_rows" > gpurun_out/ks_tests.log 2>&1 || { tail -30 gpurun_out/ks_tests.log; exit 1; }
+  -k "${KS_TESTS:-small_row_tiles or graph_replay or output_rows or batch_invariance or golden_vectors}" > gpurun_out/ks_tests.log 2>&1 || { tail -30 gpurun_out/ks_tests.log; exit 1; }
 grep -E "passed|failed" gpurun_out/ks_tests.log
 for r in $(seq "$REPS"); do
   for lib in "$@"; do
