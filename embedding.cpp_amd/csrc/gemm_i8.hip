@@ -634,6 +634,9 @@ __global__ __launch_bounds__(NW * 64) void i8_small_kernel(GemmArgs g, int n_mti
 #ifndef I8_KS
 #define I8_KS 1
 #endif
+#ifndef I8_KS_ROWS  // at most this many padded rows (one workgroup per 32 x 32 tile: at 1024 rows
+#define I8_KS_ROWS 512  // i8_small_kernel's two-wave tiles win, tools/small_rows_probe.py)
+#endif
 #ifndef I8_KS_NW48  // waves for K <= 1536 (48 / I8_KS_NW48 rounds)
 #define I8_KS_NW48 16
 #endif
@@ -848,7 +851,7 @@ static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s
     const dim3 grid(mt * nt), block(NW * 64);
     if constexpr (WT == W_Q4_0) {
         const int nkb = a.K >> 5;
-        if (I8_KS && nkb <= 96 && (epi != EPI_QKV || (a.head_dim > 0 && a.head_dim % 16 == 0 && (a.N / 3) % a.head_dim == 0))) {
+        if (I8_KS && Mpad <= I8_KS_ROWS && nkb <= 96 && (epi != EPI_QKV || (a.head_dim > 0 && a.head_dim % 16 == 0 && (a.N / 3) % a.head_dim == 0))) {
             const dim3 gk(mt * (a.N / 32));
             const int ntk = a.N / 32;
             auto go = [&](auto kern, int nw) { hipLaunchKernelGGL(kern, gk, dim3(nw * 64), 0, s, a, mt, ntk); };
