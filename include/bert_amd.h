@@ -125,8 +125,8 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
                         checks; default 0)
      "small_rows" n >= 0 batches of at most n padded rows (default 2048; one
                         sentence is 128) run the int8 GEMMs in 32-row tiles
-                        (Q4_0 with K <= 3072: the K loop split over 12-16
-                        waves; latency of small batches; 0 = never)
+                        (Q4_0, K <= 3072, <= 512 rows: the K loop split
+                        over 12-16 waves; latency of small batches; 0 = never)
      "graph_seqs" n >= 0 host batches of at most n sentences (and fewer than
                         fuse_min) replay a captured HIP graph of their launches
                         (default 0: measured no faster)
