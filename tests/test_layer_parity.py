@@ -159,5 +159,7 @@ def test_layer_by_layer_parity(case, sents, opts, model_dir):
         lv = [r[f"local_{var}_1mcos"] for r in rows if r["stage"]]
         print(f"  mean local 1-cos vs the {var} build {np.mean(lv):.2e} (max {max(lv):.2e}, "
               f"layers where the GPU equals it bit for bit: {sum(v == 0.0 for v in lv)} of {len(lv)})")
-    assert max(loc) <= 1e-5, loc
-    assert np.mean(loc) <= max(4 * np.mean(spr), 2e-7), (np.mean(loc), np.mean(spr))
+    # (measured, round 5: max local 1.6e-6 on C5; mean local / mean spread
+    # 0.83 - 1.13 across the fixtures and forms)
+    assert max(loc) <= 4e-6, loc
+    assert np.mean(loc) <= max(1.5 * np.mean(spr), 2e-7), (np.mean(loc), np.mean(spr))
