@@ -828,6 +828,7 @@ def test_small_batches_unfused_bitwise_fused(shape, ftype, model_dir):
     ("minilm", "q4_1", None, {"i8": "all", "q41bf": 1}),
     ("bge-large", "q4_1", 2, {"i8": "all"}),
     ("e5-base", "q4_0", 2, {"i8": "all"}),  # K = 768 / 3072: the K-split kernel's 2- and 6-round forms
+    ("bge-large", "q4_0", 2, {"i8": "all"}),  # K = 1024 split, K = 4096 on the two-wave tiles
 ])
 def test_small_row_tiles_bitwise(shape, ftype, n_layer, opts, model_dir):
     """Batches of at most small_rows padded rows (one server sentence: 128) run
