@@ -166,6 +166,11 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles);
 bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw);
 // n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
 hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s);
+// Small batches, Q4_0 at n_embd 384 / head dim 32, every sentence <= 128 tokens:
+// the int8 QKV of one head and its attention in one workgroup per (head,
+// sentence), bitwise the unfused pair (kernels.hip qkv_attention_small_kernel).
+// hipErrorNotSupported when the shape does not fit.
+hipError_t launch_qkv_attention_small(const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s);
 // out_row (optional): output row of each sentence (default: its batch index)
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s,
                        const int32_t *out_row = nullptr);

@@ -1282,6 +1282,157 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
     }
 }
 
+// Small batches (the server's one sentence), Q4_0, head dim 32, n_embd 384:
+// the int8 QKV projection of one head fused with its attention — one 12-wave
+// workgroup per (head, sentence).  Wave t < 3 nt (nt = the sentence's 32-row
+// tiles) computes tile (row tile t / 3, part t % 3 of the head's Q | K | V) over
+// the 12 quant blocks in block order with every operand loaded up front (the
+// i8 fold of i8_block: acc = fma(float(isum), d_w d_a, acc)), splits b + W.x
+// hi / lo (i8_small_epi's EPI_QKV arithmetic) into the head's LDS tiles (keys
+// past the sentence zero, as attention_short_kernel stages them); then waves
+// 0 .. nt - 1 run attention_short_kernel's per-head body on those tiles.  Every
+// value is the unfused pair's bit for bit; Q, K and V never leave the CU and
+// one launch per layer goes away.
+#ifndef QKVA_SMALL
+#define QKVA_SMALL 1
+#endif
+
+__global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, AttnArgs a) {
+    constexpr int D = 32, E = 384, NKB = E / 32, NK = 128, KST = D + 8, VST = NK + 4;
+    __shared__ __attribute__((aligned(16))) _Float16 Qh[NK * KST], Ql[NK * KST], Kh[NK * KST], Kl[NK * KST];
+    __shared__ __attribute__((aligned(16))) _Float16 Vh[D * VST], Vl[D * VST];
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
+    const int h = blockIdx.x, s = blockIdx.y;
+    const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
+    if (n > NK || n <= 0 || g.K != E || a.E != E) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+    const int nt = (n + 31) >> 5;
+    const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
+    for (int i = tid; i < a.expt.n_pad / 8; i += 768) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
+
+    if (wv < 3 * nt) {
+        const int rt = wv / 3, part = wv - 3 * rt, ft0 = 3 * h + part;  // head-major f-tile of Q | K | V
+        const int64_t row = beg + 32 * rt + r;                          // (rows past the batch: spare rows)
+        // operands of blocks b .. b + 5 in flight (a six-slot ring, slot b % 6)
+        constexpr int RING = 6;
+        int4v wq[RING], xa[RING];
+        uint32_t dw[RING], da[RING];
+        auto load = [&](int b) {
+            const int sl = b % RING;
+            wq[sl] = i8_wq(g.Wi, NKB, ft0, b);
+            xa[sl] = *(const int4v *)((const int8_t *)g.A.q + row * E + 32 * b + 16 * hh);
+            dw[sl] = ((const uint16_t *)g.Wi.dh)[(((int64_t)ft0 * (NKB >> 2) + (b >> 2)) * 32 + r) * 4 + (b & 3)];
+            da[sl] = ((const uint16_t *)g.A.d)[row * NKB + b];
+        };
+#pragma unroll
+        for (int b = 0; b < RING; b++) load(b);
+        const int f0 = 32 * ft0 + 16 * hh;
+        float4v b4[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) b4[q] = *(const float4v *)(g.bias + f0 + 4 * q);
+        const float16v zf = {};
+        float16v acc = {};
+#pragma unroll
+        for (int b = 0; b < NKB; b++) {
+            const int sl = b % RING;
+            const int16v is = __builtin_amdgcn_mfma_i32_32x32x32_i8(wq[sl], xa[sl], __builtin_bit_cast(int16v, zf), 0, 0, 0);
+            const int4v ws = int4v{(int)dw[sl], 0, 0, 0}, oh = int4v{hh ? 0 : (int)da[sl], 0, 0, 0};
+            const float16v dd = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, ws),
+                                                                        __builtin_bit_cast(half8, oh), zf, 0, 0, 0);
+            if (b + RING < NKB) load(b + RING);
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc[i] = __builtin_fmaf((float)is[i], dd[i], acc[i]);
+        }
+        const int key = 32 * rt + r;
+        const bool live = key < n;
+        half8 hv[2], lv[2];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const float y = b4[i >> 2][i & 3] + acc[i];
+            const _Float16 yh = (_Float16)y;
+            hv[i >> 3][i & 7] = live ? yh : (_Float16)0.f;
+            lv[i >> 3][i & 7] = live ? (_Float16)(y - (float)yh) : (_Float16)0.f;
+        }
+        if (part < 2) {
+            _Float16 *th = part ? Kh : Qh, *tl = part ? Kl : Ql;
+            *(half8 *)&th[key * KST + 16 * hh] = hv[0];
+            *(half8 *)&th[key * KST + 16 * hh + 8] = hv[1];
+            *(half8 *)&tl[key * KST + 16 * hh] = lv[0];
+            *(half8 *)&tl[key * KST + 16 * hh + 8] = lv[1];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                Vh[(16 * hh + i) * VST + key] = hv[i >> 3][i & 7];
+                Vl[(16 * hh + i) * VST + key] = lv[i >> 3][i & 7];
+            }
+        }
+    }
+    __syncthreads();
+    const int q0 = wv * 32;
+    if (q0 >= n) return;
+    // attention_short_kernel's per-head body, Q from the LDS tiles
+    half8 qh[D / 16], ql[D / 16];
+    {
+        const int qr = min(q0 + r, n - 1);
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ks++) {
+            qh[ks] = *(const half8 *)&Qh[qr * KST + 16 * ks + 8 * hh];
+            ql[ks] = *(const half8 *)&Ql[qr * KST + 16 * ks + 8 * hh];
+        }
+    }
+    const int nkt = (n + 31) >> 5;
+    float16v S[4];
+    const float16v zero16 = {};
+#pragma unroll
+    for (int kt = 0; kt < 4; kt++) S[kt] = kt < nkt ? attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql) : zero16;
+    int lim = n - 4 * hh;
+    asm volatile("" : "+v"(lim));
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; kt++) {
+        if (kt < nkt) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) S[kt][j] = S[kt][j] * a.scale;
+            if (32 * kt + 32 > n) {
+#pragma unroll
+                for (int j = 0; j < 16; j++)
+                    if (32 * kt + (j & 3) + 8 * (j >> 2) >= lim) S[kt][j] = -INFINITY;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[kt][j]);
+        }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    uint32_t sum = 0;
+#pragma unroll
+    for (int kt = 0; kt < 4; kt++) {
+        if (kt < nkt) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint32_t hm = f2h(mx - S[kt][j]);
+                const float p = h2f(etab[epos + min(hm, (uint32_t)eneg)]);
+                S[kt][j] = p;
+                sum += (uint32_t)(p * 16777216.0f);
+            }
+        }
+    }
+    sum += __shfl_xor(sum, 32);
+    const float rs = (float)(1.0 / ((double)sum * 0x1p-24));
+    float16v o[D / 32];
+#pragma unroll
+    for (int dt = 0; dt < D / 32; dt++) o[dt] = zero16;
+#pragma unroll
+    for (int kt = 0; kt < 4; kt++)
+        if (kt < nkt) attn_pv<D>(o, Vh, Vl, VST, 32 * kt, r, hh, S[kt]);
+    attn_store_ctx<W_Q4_0, D>(a, o, rs, beg + q0 + r, q0 + r < n, h, hh);
+}
+
+hipError_t launch_qkv_attention_small(const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
+    if (!QKVA_SMALL || g.K != 384 || a.E != 384 || a.H * 32 != a.E || n_seqs <= 0) return hipErrorNotSupported;
+    hipLaunchKernelGGL(qkv_attention_small_kernel, dim3(a.H, n_seqs), dim3(768), 0, s, g, a);
+    return hipGetLastError();
+}
+
 // QKV projection fused with attention, for batches whose sentences all have
 // n <= 128 tokens, heads of D = 32 (MiniLM) or 64 (e5-base, bge-large): one
 // 12-wave workgroup per sentence, so Q, K and V (hi/lo, 4 bytes a value)

@@ -293,6 +293,10 @@ struct bert_ctx {
     // one-sentence call measured 327 us eager, 332 us replayed — the device's
     // ~4.5 us per dependent kernel bounds it, not the host's launches)
     int graph_seqs = 0;
+    // small batches (<= 512 padded rows, every sentence <= 128 tokens; Q4_0 at
+    // n_embd 384, head dim 32, int8 QKV): each head's QKV and attention in one
+    // kernel (kernels.hip qkv_attention_small_kernel; bitwise the unfused pair)
+    bool small_qkva = true;
     uint64_t opt_gen = 0;  // bumped by every option change (captured graphs are dropped)
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
@@ -726,6 +730,12 @@ void i8_select(bert_ctx *ctx, const std::string &spec) {
 // group's first row; the QKV + attention kernels index rows absolutely through
 // the offsets, so they get the workspace bases (the unfused pair only runs
 // with one group, row0 == 0).
+// the fused small QKV + attention kernel computes a head's 3 x ceil(n / 32)
+// QKV tiles on one workgroup: it wins for one sentence of 16 tokens (271 vs
+// 286-314 us per call), not at 128 (311-314 vs 300-320): tools/opt_latency_ab.sh
+#ifndef QKVA_SMALL_MAX_LEN
+#define QKVA_SMALL_MAX_LEN 64
+#endif
 bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
                const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
                ActPtr Ca, ActPtr Ua, float *X, hipStream_t st) {
@@ -774,6 +784,11 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
             qf.Wi = L.qkv8;  // (qkva_ntw 0)
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
+        } else if (ctx->i8_qkv && ctx->small_qkva && small && wt8 == W_Q4_0 && E == 384 && D == 32 &&
+                   max_len <= QKVA_SMALL_MAX_LEN && rows <= 512) {
+            // one sentence (the server's path): the head's QKV and attention in one kernel
+            q.Wi = L.qkv8;
+            LAUNCH_OK("qkv_attention", launch_qkv_attention_small(q, aa, nseq, st));
         } else if (ctx->i8_qkv) {  // the int8 QKV of the producer / consumer kernel, unfused
             q.Wi = L.qkv8;
             LAUNCH_OK("gemm_qkv", gemm_i8(EPI_QKV, q));
@@ -1250,6 +1265,8 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         ctx->fuse_min = value;
     } else if (k == "unfused") {
         ctx->unfused = value != 0;
+    } else if (k == "small_qkva") {
+        ctx->small_qkva = value != 0;
     } else if (k == "small_rows" || k == "graph_seqs") {
         if (need(value >= 0, "must be >= 0")) return -2;
         (k == "small_rows" ? ctx->small_rows : ctx->graph_seqs) = value;
@@ -1272,7 +1289,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
     static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows", "graph_seqs",
-                                 "encode_lanes", "encode_merge", "encode_merge_rows"};
+                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
         std::string env = "BERT_AMD_" + std::string(k);
@@ -2299,7 +2316,7 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
     const std::string k = key;
     const std::pair<const char *, int32_t> opts[] = {
         {"split", ctx->split}, {"pack", ctx->pack}, {"fuse_min", ctx->fuse_min}, {"unfused", ctx->unfused},
-        {"small_rows", ctx->small_rows}, {"graph_seqs", ctx->graph_seqs},
+        {"small_rows", ctx->small_rows}, {"graph_seqs", ctx->graph_seqs}, {"small_qkva", ctx->small_qkva},
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
