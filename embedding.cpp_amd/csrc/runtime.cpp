@@ -736,6 +736,9 @@ void i8_select(bert_ctx *ctx, const std::string &spec) {
 #ifndef QKVA_SMALL_MAX_LEN
 #define QKVA_SMALL_MAX_LEN 64
 #endif
+#ifndef QKVA_SMALL_ROWS  // (and the batch small: rows <= small_rows) — it wins at every
+#define QKVA_SMALL_ROWS 2048  // small size, tools/qkva_batch_probe.py (16 x 48 tokens 450 vs 500 us)
+#endif
 bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
                const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
                ActPtr Ca, ActPtr Ua, float *X, hipStream_t st) {
@@ -785,7 +788,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             qf.Wi = L.qkv8;  // (qkva_ntw 0)
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
         } else if (ctx->i8_qkv && ctx->small_qkva && small && wt8 == W_Q4_0 && E == 384 && D == 32 &&
-                   max_len <= QKVA_SMALL_MAX_LEN && rows <= 512) {
+                   max_len <= QKVA_SMALL_MAX_LEN && rows <= QKVA_SMALL_ROWS) {
             // one sentence (the server's path): the head's QKV and attention in one kernel
             q.Wi = L.qkv8;
             LAUNCH_OK("qkv_attention", launch_qkv_attention_small(q, aa, nseq, st));

@@ -127,7 +127,7 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
                         sentence is 128) run the int8 GEMMs in 32-row tiles
                         (Q4_0, K <= 3072, <= 512 rows: the K loop split
                         over 12-16 waves; latency of small batches; 0 = never)
-     "small_qkva" 0 | 1  1 (default): batches of at most 512 padded rows whose
+     "small_qkva" 0 | 1  1 (default): small batches (<= small_rows, <= 2048 rows) whose
                         sentences all have <= 64 tokens (Q4_0, n_embd 384, head
                         dim 32) run each head's int8 QKV and its attention in one
                         kernel (same results; one launch less per layer)
