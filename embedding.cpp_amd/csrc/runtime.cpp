@@ -923,8 +923,15 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
     // (option "unfused" forces the two-kernel path, for A/B checks)
     // (an int8 QKV copy without the producer / consumer kernel, i8 qkv: the
     // head-pair kernel has no int8 form, so every batch takes the unfused pair)
+    // Small batches of short sentences take qkv_attention_small_kernel (run_layer)
+    // whatever their count: one workgroup per (head, sentence) against the
+    // producer / consumer kernel's one per 128-row tile (48 x 16 tokens: 575 vs
+    // 856 us per call, tools/fuse_min_probe.py)
+    const bool small_short = ctx->small_qkva && ctx->i8_qkv && !ctx->unfused && Mpad <= ctx->small_rows &&
+                             Mpad <= QKVA_SMALL_ROWS && max_len <= QKVA_SMALL_MAX_LEN && wt == W_Q4_0 && E == 384 &&
+                             E / H == 32 && !tap;
     const bool fused_qkv_attn = !ctx->unfused && n_seqs >= ctx->fuse_min && (!ctx->i8_qkv || ctx->qkva_ntw == 0) &&
-                                qkv_attention_supported(wt, E, H, max_len, ctx->qkva_ntw);
+                                qkv_attention_supported(wt, E, H, max_len, ctx->qkva_ntw) && !small_short;
 
     const EmbedArgs ea = embed_args(ctx, R, w, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(ctx->wtype, ea, (int)Mpad, st));
