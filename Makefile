@@ -11,6 +11,8 @@ INC := -Iinclude -I$(SRC)
 HOST_SRCS := gguf_io.cpp quantize.cpp quantize_model.cpp synth.cpp tokenizer.cpp runtime.cpp
 HOST_OBJS := $(addprefix $(BUILD)/obj/,$(HOST_SRCS:.cpp=.o))
 HIP_OBJS := $(BUILD)/obj/kernels.o $(BUILD)/obj/gemm_i8.o
+# the library's sources, in the order bench.py's src_hash() reads them
+SRC_HASH_FILES := $(sort $(wildcard $(SRC)/*.hip $(SRC)/*.cpp $(SRC)/*.h $(SRC)/*.inc include/*.h include/ggml/*.h)) Makefile
 CXXFLAGS := -O2 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-result \
             -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include $(INC)
 HIPFLAGS := -O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=$(ARCH) $(INC)
@@ -29,9 +31,12 @@ $(BUILD)/obj/%.o: $(SRC)/%.hip $(SRC)/kernels.h $(SRC)/kernels_common.h $(SRC)/i
 
 $(BUILD)/libbert.so: $(HOST_OBJS) $(HIP_OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
-	@# the commit this library was built from (bench.py / tools/pmc_traffic.py record it)
+	@# the commit this library was built from (bench.py / tools/pmc_traffic.py record it), and a
+	@# hash of the sources it was built from (bench.py compares it with the tree it runs in, so a
+	@# library built just before its sources were committed is still identified as their build)
 	@{ git rev-parse HEAD 2>/dev/null || echo unknown; } | tr -d '\n' > $(BUILD)/BUILD_INFO
 	@git diff --quiet HEAD -- embedding.cpp_amd include 2>/dev/null || printf ' +uncommitted' >> $(BUILD)/BUILD_INFO
+	@printf ' src=%s' "$$(cat $(SRC_HASH_FILES) | sha256sum | cut -c1-16)" >> $(BUILD)/BUILD_INFO
 
 oracle:
 	$(MAKE) -C oracle
@@ -86,7 +91,11 @@ REF ?= /root/reference
 $(BUILD)/ref_%: $(REF)/examples/%.cpp $(BUILD)/libbert.so include/bert.h include/ggml.h
 	$(CXX) -std=c++17 -O2 -Iinclude $< -o $@ -L$(BUILD) -lbert -Wl,-rpath,'$$ORIGIN'
 
-ref_consumers: $(BUILD)/ref_server $(BUILD)/ref_main
+# models/quantize.cpp (reference) includes "ggml/ggml.h": include/ggml/ggml.h is the same shim
+$(BUILD)/ref_quantize: $(REF)/models/quantize.cpp $(BUILD)/libbert.so include/bert.h include/ggml/ggml.h
+	$(CXX) -std=c++17 -O2 -Iinclude $< -o $@ -L$(BUILD) -lbert -Wl,-rpath,'$$ORIGIN'
+
+ref_consumers: $(BUILD)/ref_server $(BUILD)/ref_main $(BUILD)/ref_quantize
 .PHONY: ref_consumers
 
 # development timing of the fused kernel's phases (tools/qkva_time.hip)

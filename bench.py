@@ -132,7 +132,25 @@ def build_info() -> dict:
     if os.path.exists(bi):
         with open(bi) as f:
             info["git_head"] = f.read().strip()
+        built = [w[4:] for w in info["git_head"].split() if w.startswith("src=")]
+        if built:
+            info["src_matches_tree"] = built[0] == src_hash()
     return info
+
+
+def src_hash() -> str:
+    """sha256 (first 16 hex digits) of the library's sources in this tree, the
+    same file list and order as the Makefile's SRC_HASH_FILES."""
+    import glob
+    import hashlib
+    pats = ["embedding.cpp_amd/csrc/*.hip", "embedding.cpp_amd/csrc/*.cpp", "embedding.cpp_amd/csrc/*.h",
+            "embedding.cpp_amd/csrc/*.inc", "include/*.h", "include/ggml/*.h"]
+    files = sorted(set(os.path.relpath(f, REPO) for p in pats for f in glob.glob(os.path.join(REPO, p))))
+    h = hashlib.sha256()
+    for f in files + ["Makefile"]:
+        with open(os.path.join(REPO, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
@@ -142,7 +160,7 @@ def kernel_flops(name: str, B: int, N: int, hp: dict) -> float:
 def kernel_parts(name: str, B: int, N: int, hp: dict, arith: dict, ftype: str) -> list:
     """Algorithmic work of one launch split by the MFMA arithmetic it runs on:
     [(flops, peak TFLOP/s)].  `arith` is the library's resolved choice per
-    projection (bert_amd_get_option: qkva_ntw, i8_up / i8_o / i8_down): a Q4
+    projection (bert_amd_get_option: i8_qkv / i8_up / i8_o / i8_down): a Q4
     projection on the int8-MFMA GEMMs is priced at the int8 peak, one on the
     split-fp16 GEMMs at the fp16 peak; attention (split-fp16 K.Q and P.V) at
     the fp16 peak; F32 GEMMs at the fp32 MFMA peak."""
@@ -154,7 +172,9 @@ def kernel_parts(name: str, B: int, N: int, hp: dict, arith: dict, ftype: str) -
     def proj(key):
         return PEAK_INT8_TOPS if q4 and arith.get(key) else gemm_peak
 
-    qkv_int8 = q4 and arith.get("qkva_ntw") == 0  # producer / consumer kernel and its unfused twin
+    # i8_qkv: the producer / consumer kernel and its unfused twin, or the unfused
+    # int8 QKV GEMM of option i8=qkv (older callers pass only qkva_ntw: 0 = int8)
+    qkv_int8 = q4 and bool(arith["i8_qkv"] if "i8_qkv" in arith else arith.get("qkva_ntw") == 0)
     qkv = (2.0 * M * E * 3 * E, PEAK_INT8_TOPS if qkv_int8 else gemm_peak)
     att = (4.0 * B * N * N * E, PEAK_FP16_TFLOPS)
     return {
@@ -172,14 +192,16 @@ def dtype_label(ftype: str, arith: dict) -> str:
     projections (exact Q4 x Q8 block dots) beside split-fp16 ones and fp16
     attention."""
     if ftype in ("q4_0", "q4_1"):
-        i8 = arith.get("qkva_ntw") == 0 or any(arith.get(k) for k in ("i8_up", "i8_o", "i8_down"))
+        i8 = any(arith.get(k) for k in ("i8_qkv", "i8_up", "i8_o", "i8_down")) or (
+            "i8_qkv" not in arith and arith.get("qkva_ntw") == 0)
         return "int8+fp16" if i8 else "fp16"
     return "fp32+fp16" if ftype == "f32" else "fp16"
 
 
 def dtype_note(ftype: str, arith: dict) -> str:
     if ftype in ("q4_0", "q4_1"):
-        names = {"qkv": arith.get("qkva_ntw") == 0, "o": arith.get("i8_o"), "up": arith.get("i8_up"),
+        names = {"qkv": arith["i8_qkv"] if "i8_qkv" in arith else arith.get("qkva_ntw") == 0,
+                 "o": arith.get("i8_o"), "up": arith.get("i8_up"),
                  "down": arith.get("i8_down")}
         i8 = [k for k, v in names.items() if v]
         f16 = [k for k, v in names.items() if not v]
@@ -442,7 +464,7 @@ def main():
     prof = model.profile_read()
     model.profile(False)
     model.set_option("split", int(os.environ.get("BERT_AMD_SPLIT", "1")[:1] != "0"))
-    arith = {k: model.get_option(k) for k in ("qkva_ntw", "i8_up", "i8_o", "i8_down")}
+    arith = {k: model.get_option(k) for k in ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf")}
     kern = {}
     for name, (ms, cnt) in prof.items():
         parts = kernel_parts(name, B, N, hp, arith, args.ftype)

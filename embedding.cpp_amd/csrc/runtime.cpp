@@ -787,7 +787,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
             qf.Wi = L.qkv8;  // (qkva_ntw 0)
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
-        } else if (ctx->i8_qkv && ctx->small_qkva && small && wt8 == W_Q4_0 && E == 384 && D == 32 &&
+        } else if (ctx->i8_qkv && ctx->small_qkva && !ctx->unfused && small && wt8 == W_Q4_0 && E == 384 && D == 32 &&
                    max_len <= QKVA_SMALL_MAX_LEN && rows <= QKVA_SMALL_ROWS) {
             // one sentence (the server's path): the head's QKV and attention in one kernel
             q.Wi = L.qkv8;

@@ -148,10 +148,12 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
 BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int32_t value);
 
 /* Reads an option back into *value: every bert_amd_set_option key, plus the
-   load-time choices as resolved for this model — "qkva_ntw" (0, 1 or 2) and
-   "i8_up", "i8_o", "i8_down" (1 when that Q4 projection runs on the
-   int8-MFMA GEMMs).  Lets bench.py price each kernel on the arithmetic it
-   runs.  Returns 0, or -2 on an unknown key. */
+   load-time choices as resolved for this model — "qkva_ntw" (0, 1 or 2),
+   "i8_qkv", "i8_up", "i8_o", "i8_down" (1 when that Q4 projection runs on
+   the int8-MFMA GEMMs: for QKV, the producer / consumer kernel's int8 copy
+   and its unfused int8 twin) and "q41bf" (1 when Q4_1's scale products run
+   on the bf16 MFMA, W_Q4_1B).  Lets bench.py price each kernel on the
+   arithmetic it runs.  Returns 0, or -2 on an unknown key. */
 BERT_API int32_t bert_amd_get_option(struct bert_ctx *ctx, const char *key, int32_t *value);
 
 /* How bert_eval_batch splits a batch over n_replicas devices: contiguous

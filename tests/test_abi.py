@@ -152,15 +152,50 @@ def test_load_rejects_bad_files(model_dir):
 REF = "/root/reference"
 
 
+def _compile_ref(repo, src, out, extra=("-L", None, "-lbert")):
+    cmd = ["g++", "-std=c++17", "-O1", "-I", os.path.join(repo, "include"), src, "-o", str(out)]
+    if extra:
+        cmd += ["-L", os.path.join(repo, "build"), "-lbert", "-Wl,-rpath," + os.path.join(repo, "build")]
+    else:
+        cmd += ["-ldl"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, (src, r.stderr[-2000:])
+
+
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "examples")), reason="reference checkout absent")
 def test_reference_consumers_compile_unchanged(repo, tmp_path):
-    """examples/main.cpp and server.cpp (reference) build against include/ and link build/libbert.so."""
-    for ex in ["main.cpp", "server.cpp", "test_tokenizer.cpp"]:
-        out = tmp_path / ex.replace(".cpp", "")
-        r = subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(repo, "include"),
-                            os.path.join(REF, "examples", ex), "-o", str(out), "-L", os.path.join(repo, "build"),
-                            "-lbert", "-Wl,-rpath," + os.path.join(repo, "build")], capture_output=True, text=True)
+    """The reference's consumer programs build unchanged against include/ and
+    link build/libbert.so: examples/main.cpp, server.cpp, test_tokenizer.cpp,
+    test_embedding.cpp (bert.h + ggml.h), models/quantize.cpp (includes
+    "ggml/ggml.h", reference models/quantize.cpp:1) and examples/dylib.cpp
+    (dlopen's the library by path, reference examples/dylib.cpp:8: no link)."""
+    for ex in ["main.cpp", "server.cpp", "test_tokenizer.cpp", "test_embedding.cpp"]:
+        _compile_ref(repo, os.path.join(REF, "examples", ex), tmp_path / ex.replace(".cpp", ""))
+    _compile_ref(repo, os.path.join(REF, "models", "quantize.cpp"), tmp_path / "quantize")
+    _compile_ref(repo, os.path.join(REF, "examples", "dylib.cpp"), tmp_path / "dylib", extra=None)
+
+
+@pytest.mark.skipif(not os.path.isfile(os.path.join(REF, "models", "quantize.cpp")), reason="reference checkout absent")
+def test_reference_quantize_program_equals_library_quantiser(repo, model_dir, tmp_path):
+    """The reference's own quantize program (models/quantize.cpp, compiled
+    unchanged, whose work is bert_model_quantize: models/quantize.cpp:47) run on
+    an f32 GGUF writes the same bytes as bert_model_quantize called through
+    ctypes, for q4_0 and q4_1 (type 2 / 3, models/quantize.cpp:23-24); a bad
+    type fails with exit code 1 as in the reference."""
+    exe = tmp_path / "quantize"
+    _compile_ref(repo, os.path.join(REF, "models", "quantize.cpp"), exe)
+    f32 = os.path.join(model_dir, "refq_src_f32.gguf")
+    bertlib.synth_model(f32, "minilm", "f32", n_layer=1, seed=11)
+    for ftype, code in (("q4_0", "2"), ("q4_1", "3")):
+        via_prog = tmp_path / f"prog_{ftype}.gguf"
+        via_lib = tmp_path / f"lib_{ftype}.gguf"
+        r = subprocess.run([str(exe), f32, str(via_prog), code], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-2000:]
+        assert "quantize time" in r.stdout
+        assert bertlib.quantize(f32, str(via_lib), ftype)
+        assert via_prog.read_bytes() == via_lib.read_bytes(), ftype
+    r = subprocess.run([str(exe), f32, str(tmp_path / "bad.gguf"), "7"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1
 
 
 @pytest.mark.parametrize("n_rep", [1, 2, 3, 8])

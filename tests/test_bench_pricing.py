@@ -41,3 +41,19 @@ def test_projection_forms_follow_the_library():
     assert bench.dtype_label("q4_0", PC) == "int8+fp16"
     assert bench.dtype_label("f16", {}) == "fp16"
     assert "qkv/up/down on int8 MFMA" in bench.dtype_note("q4_0", PC)
+
+
+def test_int8_qkv_gemm_priced_by_resolved_choice():
+    """option i8=qkv puts the unfused QKV GEMM on the int8 MFMA with
+    the head-pair fused kernel (qkva_ntw != 0); the library reports it as
+    i8_qkv, and bench prices it at the int8 peak (qkva_ntw alone would say fp16)."""
+    arith = {"qkva_ntw": 2, "i8_qkv": 1, "i8_up": 1, "i8_o": 0, "i8_down": 0}
+    assert bench.kernel_parts("gemm_qkv", 8, 512, bertlib.SHAPES["bge-large"], arith, "q4_1")[0][1] == \
+        bench.PEAK_INT8_TOPS
+    assert "qkv/up on int8 MFMA" in bench.dtype_note("q4_1", arith)
+    off = dict(arith, i8_qkv=0, i8_up=0)
+    assert bench.kernel_parts("gemm_qkv", 8, 512, bertlib.SHAPES["bge-large"], off, "q4_1")[0][1] == \
+        bench.PEAK_FP16_TFLOPS
+    assert bench.dtype_label("q4_1", off) == "fp16"
+    # the pc kernel reports i8_qkv = 1 with qkva_ntw = 0
+    assert bench.kernel_parts("gemm_qkv", 8, 128, HP, dict(PC, i8_qkv=1), "q4_0")[0][1] == bench.PEAK_INT8_TOPS

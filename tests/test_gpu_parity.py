@@ -821,6 +821,30 @@ def test_small_batches_unfused_bitwise_fused(shape, ftype, model_dir):
     assert np.array_equal(m.eval(toks[5]), fused[5])
 
 
+def test_unfused_option_covers_the_small_kernel(model_dir):
+    """Option "unfused" runs every batch on the QKV GEMM + attention pair
+    (bert_amd.h), including the small batches that otherwise take the fused
+    small QKV + attention kernel: the per-kernel profile of a
+    16-token sentence names gemm_qkv + attention with it and qkv_attention
+    without it, and the embeddings are bitwise the same."""
+    p, m = get_model(model_dir, "minilm", "q4_0")
+    toks = [sentence(901, 16, 30522)]
+    try:
+        m.profile(True)  # enabling clears the accumulated times
+        fused = m.eval_batch(toks)
+        kf = m.profile_read()
+        m.set_option("unfused", 1)
+        m.profile(True)
+        unfused = m.eval_batch(toks)
+        ku = m.profile_read()
+    finally:
+        m.set_option("unfused", 0)
+        m.profile(False)
+    assert "qkv_attention" in kf and "gemm_qkv" not in kf, kf
+    assert "gemm_qkv" in ku and "attention" in ku and "qkv_attention" not in ku, ku
+    assert np.array_equal(fused, unfused)
+
+
 @pytest.mark.parametrize("shape,ftype,n_layer,opts", [
     ("minilm", "q4_0", None, {}),
     ("minilm", "q4_0", None, {"i8": "all"}),
