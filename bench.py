@@ -356,6 +356,8 @@ def main():
     ap.add_argument("--w-std", type=float, default=0.05)
     ap.add_argument("--model-dir", default=os.environ.get("BERT_AMD_MODEL_DIR", "/tmp/bert_amd_models"))
     ap.add_argument("--cpu-sample", type=int, default=256, help="sentences for the CPU oracle baseline (0: skip)")
+    ap.add_argument("--cpu-sample-scalar", type=int, default=64,
+                    help="of those, sentences for the scalar form of the oracle (timed beside the SIMD form)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--pmc-csv", default=os.environ.get("BENCH_PMC_CSV", ""))
@@ -663,20 +665,43 @@ def main():
         orc = oracle.Oracle(path)
         sample = [toks[i].tolist() for i in range(S)]
         orc.eval_batch(sample[:1], threads)  # warm-up (page-in of the model file)
-        c0 = time.perf_counter()
-        ref = orc.eval_batch(sample, threads)
-        c1 = time.perf_counter()
         cpu_model = ""
         try:
             with open("/proc/cpuinfo") as f:
                 cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
         except OSError:
             pass
-        cpu = dict(value=round(S / (c1 - c0), 3), unit="embeddings/s", cores=threads, kind="port",
-                   sample=f"first {S} of the {B} sentences (seq_len {N}), oracle/bert_oracle.c "
-                          f"(ggml-semantics C restatement, scalar C, not ggml's SIMD kernels; one sentence at a "
-                          f"time, {threads} OpenMP threads = the CPU share of this job, -O3 -march=x86-64-v3)",
-                   seconds=round(c1 - c0, 2), cpu_model=cpu_model, host_cpus=os.cpu_count())
+        # the scalar AVX2-order checker on a smaller sample (it is 5-7x slower), then the same
+        # checker in AVX2 intrinsics (ggml's AVX2 instructions, bitwise equal:
+        # tests/test_oracle.py::test_simd_oracle_bitwise_scalar) on the whole sample
+        Ss = max(1, min(S, args.cpu_sample_scalar))
+        c0 = time.perf_counter()
+        ref_s = orc.eval_batch(sample[:Ss], threads)
+        c1 = time.perf_counter()
+        scalar = dict(value=round(Ss / (c1 - c0), 3), unit="embeddings/s", cores=threads, kind="port",
+                      sample=f"first {Ss} of the {B} sentences, scalar C form of the checker",
+                      seconds=round(c1 - c0, 2))
+        simd = oracle.simd_available()
+        if simd:
+            oracle.set_simd(True)
+            try:
+                c0 = time.perf_counter()
+                ref = orc.eval_batch(sample, threads)
+                c1 = time.perf_counter()
+            finally:
+                oracle.set_simd(False)
+            cpu = dict(value=round(S / (c1 - c0), 3), unit="embeddings/s", cores=threads, kind="port",
+                       form="simd restatement",
+                       sample=f"first {S} of the {B} sentences (seq_len {N}), oracle/bert_oracle.c in AVX2 "
+                              f"intrinsics (ggml's AVX2 vec_dot instructions: maddubs/madd/cvt/fma per Q4 block, "
+                              f"8-lane f32 fma dots, F16C; bitwise the scalar checker), one sentence at a time, "
+                              f"{threads} OpenMP threads = the CPU share of this job, -O3 -march=x86-64-v3",
+                       seconds=round(c1 - c0, 2), cpu_model=cpu_model, host_cpus=os.cpu_count(), scalar=scalar,
+                       simd_bitwise_scalar=bool(np.array_equal(ref[:Ss], ref_s)))
+        else:
+            ref = ref_s
+            S = Ss
+            cpu = dict(scalar, cpu_model=cpu_model, host_cpus=os.cpu_count(), form="scalar restatement")
         a = out[:S].astype(np.float64)
         c = (a * ref).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(ref, axis=1)
         parity = dict(cos_min=float(c.min()), cos_mean=float(c.mean()), n=S,

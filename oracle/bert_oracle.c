@@ -44,6 +44,7 @@
 #ifdef _OPENMP
 #include <omp.h>
 #endif
+#include <immintrin.h>
 
 #define QK 32
 enum { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q4_1 = 3 };
@@ -85,8 +86,13 @@ float oracle_f16_to_f32(uint16_t h) {
     return bitsf(b);
 }
 
-static float F16(uint16_t h) { return oracle_f16_to_f32(h); }
-static uint16_t H16(float f) { return oracle_f32_to_f16(f); }
+static int g_simd = 0; /* the AVX2-intrinsics form of the checker (oracle_set_simd, below) */
+/* fp16 <-> f32: the bit-exact software conversions, or F16C's vcvtps2ph (round
+   to nearest even) / vcvtph2ps in the SIMD form — the same values for every
+   non-NaN input (tests/test_oracle.py::test_fp16_conversion_bit_exact,
+   ::test_simd_oracle_bitwise_scalar) */
+static float F16(uint16_t h) { return g_simd ? _cvtsh_ss(h) : oracle_f16_to_f32(h); }
+static uint16_t H16(float f) { return g_simd ? (uint16_t)_cvtss_sh(f, _MM_FROUND_TO_NEAREST_INT) : oracle_f32_to_f16(f); }
 
 /* ggml_init builds these once (fp16 in, fp16 out). */
 static uint16_t g_tab_gelu[65536], g_tab_exp[65536];
@@ -510,6 +516,98 @@ static float dot_q4_rows(int n, const int8_t *wq, const float *wd, const float *
     return wm ? hsum8(acc) + summs : hsum8(acc);
 }
 
+/* ----------------------------------------------------- AVX2 intrinsics
+   The same AVX2-order checker (variant 0) written with the instructions
+   ggml's AVX2 build runs (reference CMakeLists.txt:164-177 builds ggml with
+   -mavx2 -mfma -mf16c; ggml.c ggml_vec_dot_q4_0_q8_0 / _q4_1_q8_1 /
+   ggml_vec_dot_f32 / _f16, AVX2 branches): per Q4 block
+   sign/maddubs/madd give the 8 lanes of 4-product integer sums, cvt, one
+   vfmadd per lane into 8-lane accumulators; f32 dots on 4 x 8-lane fma
+   accumulators.  Every lane operation is the scalar variant-0 code's own
+   (same fma, same adds in the same order), so results are bitwise the
+   scalar checker's (tests/test_oracle.py::test_simd_oracle_bitwise_scalar);
+   it exists to time the CPU baseline at ggml's SIMD speed (bench.py
+   cpu_baseline).  Off by default (oracle_set_simd). */
+void oracle_set_simd(int on) { g_simd = on; }
+int oracle_simd_available(void) {
+    return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma") && __builtin_cpu_supports("f16c");
+}
+
+static inline float hsum8_v(__m256 v) {
+    float a[8];
+    _mm256_storeu_ps(a, v);
+    return hsum8(a);
+}
+
+/* = dot_f32_rows */
+static float dot_f32_rows_avx2(int n, const float *x, const float *y) {
+    __m256 a0 = _mm256_setzero_ps(), a1 = a0, a2 = a0, a3 = a0;
+    const int np = n & ~31;
+    for (int i = 0; i < np; i += 32) {
+        a0 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i), _mm256_loadu_ps(y + i), a0);
+        a1 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 8), _mm256_loadu_ps(y + i + 8), a1);
+        a2 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 16), _mm256_loadu_ps(y + i + 16), a2);
+        a3 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 24), _mm256_loadu_ps(y + i + 24), a3);
+    }
+    a0 = _mm256_add_ps(a0, a2);
+    a1 = _mm256_add_ps(a1, a3);
+    a0 = _mm256_add_ps(a0, a1);
+    float t[8];
+    _mm256_storeu_ps(t, a0);
+    float r4[4];
+    for (int l = 0; l < 4; l++) r4[l] = t[l + 4] + t[l];
+    return (r4[0] + r4[1]) + (r4[2] + r4[3]);
+}
+/* = dot_f32 variant 0 (rows part, then the fma tail) */
+static float dot_f32_avx2(int n, const float *x, const float *y) {
+    float sumf = dot_f32_rows_avx2(n, x, y);
+    for (int i = n & ~31; i < n; i++) sumf = fmaf(x[i], y[i], sumf);
+    return sumf;
+}
+/* the attention / pool dots: the SIMD form when it is on (variant 0 only) */
+static float dot_f32_any(int n, const float *x, const float *y) {
+    return (g_simd && g_dot_variant == 0) ? dot_f32_avx2(n, x, y) : dot_f32(n, x, y);
+}
+
+/* = dot_q4_rows for NT consecutive tokens (their Q8 rows K apart, scales
+   K / QK apart): one weight block load serves the tokens.  NT is a
+   compile-time constant in the hot call (8 accumulators in registers). */
+#define Q4_NT 8
+static inline __attribute__((always_inline)) void q4_rows_avx2_n(const int NT, int K, const int8_t *wq,
+                                                                 const float *wd, const float *wm, const float *ad,
+                                                                 const float *as, const int8_t *aq, float *out) {
+    const int nb = K / QK;
+    __m256 acc[Q4_NT];
+    float summs[Q4_NT];
+    for (int j = 0; j < NT; j++) { acc[j] = _mm256_setzero_ps(); summs[j] = 0.0f; }
+    const __m256i ones = _mm256_set1_epi16(1);
+    for (int b = 0; b < nb; b++) {
+        const __m256i w = _mm256_loadu_si256((const __m256i *)(wq + b * QK));
+        const __m256i aw = _mm256_sign_epi8(w, w); /* |w| as unsigned bytes */
+        const float wdb = wd[b];
+        for (int j = 0; j < NT; j++) {
+            const float d = wdb * ad[(size_t)j * nb + b];
+            if (wm) summs[j] += wm[b] * as[(size_t)j * nb + b];
+            const __m256i a = _mm256_loadu_si256((const __m256i *)(aq + (size_t)j * K + b * QK));
+            const __m256i p16 = _mm256_maddubs_epi16(aw, _mm256_sign_epi8(a, w)); /* |w| * (a sign w), pairs */
+            const __m256i p32 = _mm256_madd_epi16(p16, ones);                      /* lane l: bytes 4l .. 4l + 3 */
+            acc[j] = _mm256_fmadd_ps(_mm256_set1_ps(d), _mm256_cvtepi32_ps(p32), acc[j]);
+        }
+    }
+    for (int j = 0; j < NT; j++) out[j] = wm ? hsum8_v(acc[j]) + summs[j] : hsum8_v(acc[j]);
+}
+static void dot_q4_rows_avx2(int K, const int8_t *wq, const float *wd, const float *wm, const float *ad,
+                             const float *as, const int8_t *aq, int nt, float *out) {
+    if (nt == Q4_NT) {
+        if (wm) q4_rows_avx2_n(Q4_NT, K, wq, wd, wm, ad, as, aq, out);
+        else q4_rows_avx2_n(Q4_NT, K, wq, wd, NULL, ad, NULL, aq, out);
+    } else {
+        for (int j = 0; j < nt; j++)
+            q4_rows_avx2_n(1, K, wq, wd, wm, ad + (size_t)j * (K / QK), wm ? as + (size_t)j * (K / QK) : NULL,
+                           aq + (size_t)j * K, out + j);
+    }
+}
+
 /* out[t][n] = bias[n] + (W . x_t)   — ggml_add(repeat(b), mul_mat(W, x)) */
 static void mul_mat_bias(const gtensor *W, const gtensor *bias, const act_t *a, int N, float *out) {
     const int K = (int)W->ne[0], NO = (int)W->ne[1];
@@ -561,6 +659,33 @@ static void mul_mat_bias(const gtensor *W, const gtensor *bias, const act_t *a, 
                         wq[bb * QK + j + 16] = (int8_t)((blk[off + j] >> 4) - (q1 ? 0 : 8));
                     }
                 }
+            }
+            if (g_simd && (W->type == T_Q4_0 || W->type == T_Q4_1)) {
+                const int q1 = W->type == T_Q4_1;
+                for (int t = 0; t < N; t += Q4_NT) {
+                    const int nt = N - t < Q4_NT ? N - t : Q4_NT;
+                    float v[Q4_NT];
+                    dot_q4_rows_avx2(K, wq, wd, q1 ? wm : NULL, a->d + (size_t)t * (K / QK),
+                                     q1 ? a->s + (size_t)t * (K / QK) : NULL, a->q + (size_t)t * K, nt, v);
+                    for (int j = 0; j < nt; j++) out[(size_t)(t + j) * NO + n] = b[n] + v[j];
+                }
+                continue;
+            }
+            if (g_simd) {
+                for (int t = 0; t < N; t++) {
+                    float v;
+                    if (W->type == T_F32) {
+                        v = dot_f32_avx2(K, (const float *)wr, a->f + (size_t)t * K);
+                    } else { /* = dot_f16_rows */
+                        const float *y = hx + (size_t)t * K;
+                        const int np = K & ~31;
+                        double sumf = (double)dot_f32_rows_avx2(np, wf, y);
+                        for (int i = np; i < K; i++) sumf += (double)(wf[i] * y[i]);
+                        v = (float)sumf;
+                    }
+                    out[(size_t)t * NO + n] = b[n] + v;
+                }
+                continue;
             }
             for (int t = 0; t < N; t++) {
                 float v;
@@ -687,7 +812,7 @@ static void encoder_layer(const omodel *m, int il, float *x, int N) {
         for (int q = 0; q < N; q++) {
             float mx = -INFINITY;
             for (int k = 0; k < N; k++) {
-                const float s = g_attn_form == 1 ? dot_split(D, kh + k * D, qh + q * D) : dot_f32(D, kh + k * D, qh + q * D);
+                const float s = g_attn_form == 1 ? dot_split(D, kh + k * D, qh + q * D) : dot_f32_any(D, kh + k * D, qh + q * D);
                 P[k] = s * kq_scale;  /* mul_mat(K,Q), scale */
                 mx = P[k] > mx ? P[k] : mx;
             }
@@ -708,7 +833,7 @@ static void encoder_layer(const omodel *m, int il, float *x, int N) {
                 continue;
             }
             for (int k = 0; k < N; k++) P[k] *= r;
-            for (int j = 0; j < D; j++) ctx[(size_t)q * E + h * D + j] = dot_f32(N, vt + (size_t)j * N, P);
+            for (int j = 0; j < D; j++) ctx[(size_t)q * E + h * D + j] = dot_f32_any(N, vt + (size_t)j * N, P);
         }
         free(kh); free(qh); free(vt); free(P);
     }
@@ -740,7 +865,7 @@ static void pool_l2(const omodel *m, const float *x, int N, float *out) {
     for (int t = 0; t < N; t++) inv[t] = invN;
     for (int e = 0; e < E; e++) {
         for (int t = 0; t < N; t++) col[t] = x[(size_t)t * E + e];
-        out[e] = dot_f32(N, col, inv);
+        out[e] = dot_f32_any(N, col, inv);
     }
     double ss = 0.0;
     for (int e = 0; e < E; e++) ss += (double)(out[e] * out[e]);

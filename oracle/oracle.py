@@ -55,6 +55,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_max_threads.restype = ctypes.c_int
         L.oracle_set_dot_variant.argtypes = [ctypes.c_int]
         L.oracle_set_attn_form.argtypes = [ctypes.c_int]
+        L.oracle_set_simd.argtypes = [ctypes.c_int]
+        L.oracle_simd_available.restype = ctypes.c_int
         L.oracle_embed_ln.restype = ctypes.c_int
         L.oracle_embed_ln.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_float)]
@@ -84,6 +86,19 @@ def set_attn_form(name: str) -> None:
 
 def set_dot_variant(name: str) -> None:
     lib().oracle_set_dot_variant(DOT_VARIANTS[name])
+
+
+def simd_available() -> bool:
+    """The host CPU runs the AVX2 / FMA / F16C intrinsics form (bert_oracle.c oracle_set_simd)."""
+    return bool(lib().oracle_simd_available())
+
+
+def set_simd(on: bool) -> None:
+    """The AVX2-order checker written with AVX2 intrinsics (bitwise the scalar
+    form; only the CPU baseline's speed changes).  Off by default."""
+    if on and not simd_available():
+        raise RuntimeError("host CPU lacks AVX2/FMA/F16C")
+    lib().oracle_set_simd(1 if on else 0)
 
 
 class Oracle:

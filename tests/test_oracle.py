@@ -158,3 +158,25 @@ def test_ggml_order_spread_reproduces(case, model_dir):
     np.testing.assert_allclose(got, meta["ggml_order_spread_1mcos"], rtol=1e-9, atol=1e-15)
     assert np.array_equal(oracle.Oracle(p).eval_batch(toks, 0), want)
     assert max(got) > 0.0  # the orders really differ
+
+
+@pytest.mark.skipif(not oracle.simd_available(), reason="host CPU lacks AVX2/FMA/F16C")
+@pytest.mark.parametrize("case", ["c1_minilm_f32", "c2_minilm_f16", "c3_minilm_q4_0", "minilm_q4_1",
+                                  "c3_minilm_q4_0_ragged"])
+def test_simd_oracle_bitwise_scalar(case, model_dir):
+    """The AVX2-intrinsics form of the checker (bert_oracle.c oracle_set_simd:
+    ggml's AVX2 instructions, the CPU baseline bench.py times) gives the scalar
+    AVX2-order checker's embeddings bit for bit — every golden fixture's
+    stored vectors — on every weight type, including sentence lengths that are
+    not multiples of 32 (the f32 dots' fma tails) and of 4 (the Q4 path's
+    4-token groups)."""
+    meta, toks, emb = load_case(case)
+    p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    o = oracle.Oracle(p)
+    try:
+        oracle.set_simd(True)
+        got = o.eval_batch(toks, 3)
+    finally:
+        oracle.set_simd(False)
+    assert np.array_equal(got, emb)
+    assert np.array_equal(o.eval_batch(toks[:2], 3), emb[:2])  # scalar again after switching back
