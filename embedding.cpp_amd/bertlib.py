@@ -304,7 +304,7 @@ class BertModel:
 
     def get_option(self, key: str) -> int:
         """bert_amd_get_option: a pipeline option, or a resolved load-time choice
-        ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf")."""
+        ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf_up", "q41bf_down")."""
         v = ctypes.c_int32(0)
         if self.lib.bert_amd_get_option(self.ctx, key.encode(), ctypes.byref(v)) != 0:
             raise ValueError(f"bert_amd_get_option({key}) failed: {last_error()}")

@@ -265,8 +265,10 @@ struct bert_ctx {
     // which Q4 projections run on the int8-MFMA GEMMs (gemm_i8.hip; i8_select)
     bool i8_qkv = false, i8_o = false, i8_down = false, i8_up = false;
     // Q4_1 int8 GEMMs: scale products on the bf16 MFMA (kernels.h W_Q4_1B) or
-    // the f32 MFMA (load option "q41bf")
-    bool q41bf = false;
+    // the f32 MFMA (load option "q41bf"): 1 every int8
+    // projection, 0 none, -1 (default) every one but the 384-wide FFN-down +
+    // LN kernel (i8_ln384_kernel), where the bf16 part operands spill
+    int q41bf = -1;
     // the fused QKV + attention kernel's form, fixed at load: 1 or 2 = the
     // head-pair kernel with that many 192-feature units per main loop (the tile
     // grouping of its QKV weight copy), 0 = the producer / consumer kernel on an
@@ -739,17 +741,26 @@ void i8_select(bert_ctx *ctx, const std::string &spec) {
 #ifndef QKVA_SMALL_ROWS  // (and the batch small: rows <= small_rows) — it wins at every
 #define QKVA_SMALL_ROWS 2048  // small size, tools/qkva_batch_probe.py (16 x 48 tokens 450 vs 500 us)
 #endif
+// Q4_1's scale products on the bf16 MFMA for this int8 epilogue (option q41bf):
+// by default everywhere but the 384-wide FFN-down + LN kernel (measured, round
+// 6: C5 FFN-up 8.78 -> 7.62 ms, MiniLM Q4_1 FFN-up 366 -> 326 us, but its
+// i8_ln384 FFN-down 366 -> 443 us)
+static bool q41bf_for(int opt, int epi) { return opt > 0 || (opt < 0 && epi != EPI_LN); }
+
 bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
                const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
                ActPtr Ca, ActPtr Ua, float *X, hipStream_t st) {
     const HParams &hp = ctx->hp;
     Workspace &w = ln.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
-    const int wt8 = (wt == W_Q4_1 && ctx->q41bf) ? W_Q4_1B : wt;  // the int8 GEMMs' weight form
+    // the int8 GEMMs' weight form per epilogue (the same for the batch and the
+    // small-batch kernels, so their results stay bitwise equal)
+    auto wt8 = [&](int epi) { return wt == W_Q4_1 && q41bf_for(ctx->q41bf, epi) ? W_Q4_1B : wt; };
     // small batches: the int8 GEMMs in 32-row tiles (bitwise the same results)
     const bool small = rows <= ctx->small_rows;
     auto gemm_i8 = [&](int epi, const GemmArgs &a) {
-        return small ? launch_gemm_i8_small(wt8, epi, a, (int)rows, st) : launch_gemm_i8(wt8, epi, a, (int)rows, st);
+        return small ? launch_gemm_i8_small(wt8(epi), epi, a, (int)rows, st)
+                     : launch_gemm_i8(wt8(epi), epi, a, (int)rows, st);
     };
     if (!fused_qkv_attn && row0 != 0) {
         set_err("internal: unfused attention with a row split");
@@ -787,7 +798,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
             qf.Wi = L.qkv8;  // (qkva_ntw 0)
             LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
-        } else if (ctx->i8_qkv && ctx->small_qkva && !ctx->unfused && small && wt8 == W_Q4_0 && E == 384 && D == 32 &&
+        } else if (ctx->i8_qkv && ctx->small_qkva && !ctx->unfused && small && wt == W_Q4_0 && E == 384 && D == 32 &&
                    max_len <= QKVA_SMALL_MAX_LEN && rows <= QKVA_SMALL_ROWS) {
             // one sentence (the server's path): the head's QKV and attention in one kernel
             q.Wi = L.qkv8;
@@ -1340,11 +1351,11 @@ bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
             }
             ctx->qkva_ntw = (int)v;
         } else if (p.first == "q41bf") {
-            if (v < 0 || v > 1) {
-                set_err("bert_amd option q41bf: must be 0 or 1");
+            if (v < -1 || v > 1) {
+                set_err("bert_amd option q41bf: must be -1 (auto), 0 or 1");
                 return false;
             }
-            ctx->q41bf = v != 0;
+            ctx->q41bf = (int)v;
         } else if (apply_option(ctx, p.first, (int32_t)v) != 0) {
             return false;
         }
@@ -2330,7 +2341,11 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
-        {"q41bf", ctx->q41bf}};
+        {"q41bf", ctx->q41bf},
+        // resolved: FFN-up / FFN-down on the bf16 scale products (Q4_1 on the int8 GEMMs)
+        {"q41bf_up", ctx->wtype == W_Q4_1 && ctx->i8_up && q41bf_for(ctx->q41bf, EPI_GELU_ACT)},
+        {"q41bf_down", ctx->wtype == W_Q4_1 && ctx->i8_down &&
+                           q41bf_for(ctx->q41bf, ctx->hp.n_embd == 384 ? EPI_LN : EPI_RESID)}};
     for (const auto &o : opts)
         if (k == o.first) {
             *value = o.second;

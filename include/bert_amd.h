@@ -40,6 +40,11 @@ BERT_API struct bert_ctx *bert_amd_load(const char *fname, const int32_t *device
                 waves on an int8 QKV copy (Q4_0, head dim 32, n_embd 384;
                 elsewhere 1), 1 | 2 head-pair units per main loop of the
                 head-pair kernel, -1 (default) 0 where it exists, else 2
+     "q41bf"    Q4_1 on the int8 GEMMs: the per-block scale products d_w d_a
+                and m_w s_a as exact bf16 partial products on the bf16 MFMA
+                (kernels.h W_Q4_1B) instead of the f32 MFMA: 1 every int8
+                projection, 0 none, -1 (default) all but the 384-wide FFN-down
+                + LayerNorm kernel (where they cost more than they save)
    and every bert_amd_set_option key below.  Returns NULL on error (an unknown
    key or a bad value included). */
 BERT_API struct bert_ctx *bert_amd_load_opts(const char *fname, const int32_t *devices, int32_t n_devices,
@@ -151,8 +156,9 @@ BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int3
    load-time choices as resolved for this model — "qkva_ntw" (0, 1 or 2),
    "i8_qkv", "i8_up", "i8_o", "i8_down" (1 when that Q4 projection runs on
    the int8-MFMA GEMMs: for QKV, the producer / consumer kernel's int8 copy
-   and its unfused int8 twin) and "q41bf" (1 when Q4_1's scale products run
-   on the bf16 MFMA, W_Q4_1B).  Lets bench.py price each kernel on the
+   and its unfused int8 twin), "q41bf" (the load option: -1 auto, 0, 1) and
+   "q41bf_up", "q41bf_down" (1 when that Q4_1 projection's scale products
+   run on the bf16 MFMA, W_Q4_1B).  Lets bench.py price each kernel on the
    arithmetic it runs.  Returns 0, or -2 on an unknown key. */
 BERT_API int32_t bert_amd_get_option(struct bert_ctx *ctx, const char *key, int32_t *value);
 

@@ -253,6 +253,18 @@ def test_q41_bf16_scale_products(case, model_dir):
     assert cos(got, ref).min() >= COS_TOL
 
 
+def test_q41bf_default_resolution(model_dir):
+    """The q41bf default (-1) puts Q4_1's scale products on the bf16 MFMA in
+    FFN-up but not in the 384-wide FFN-down + LN kernel (runtime.cpp
+    q41bf_for), and the batch / small-batch kernels take
+    the same form (bitwise equal, test_small_row_tiles_bitwise)."""
+    p, m = get_model(model_dir, "minilm", "q4_1")
+    assert m.get_option("q41bf") == -1
+    assert m.get_option("q41bf_up") == 1 and m.get_option("q41bf_down") == 0
+    p0, m0 = get_model(model_dir, "minilm", "q4_0")
+    assert m0.get_option("q41bf_up") == 0 and m0.get_option("q41bf_down") == 0
+
+
 def test_bf16_split_scale_product_probe():
     """tools/mfma_bf16_split_probe.hip: how v_mfma_f32_32x32x16_bf16 rounds a
     sum of six exact bf16 partial products (the q41bf scale products) against

@@ -60,11 +60,16 @@ CASES = [
     ("c2_minilm_f16", [0], {"fuse_min": 0}),
     ("minilm_q4_1", [0, 1], {"fuse_min": 0}),
     ("c5_bge_q4_1", [0], {}),
+    # Q4_1's scale products on the bf16 MFMA (W_Q4_1B) held to the same acceptance
+    ("c5_bge_q4_1", [0], {"q41bf": 1}),
+    ("minilm_q4_1", [0, 1], {"fuse_min": 0, "q41bf": 1}),
+    ("c5_bge_q4_1", [0], {"q41bf": 0}),
 ]
 
 
 def _tag(c):
-    return c[0] + ("-i8all" if c[2].get("i8") == "all" else "-fused" if c[2].get("fuse_min") == 0 else "-pair")
+    t = c[0] + ("-i8all" if c[2].get("i8") == "all" else "-fused" if c[2].get("fuse_min") == 0 else "-pair")
+    return t + (f"-q41bf{c[2]['q41bf']}" if "q41bf" in c[2] else "")
 
 
 @pytest.mark.parametrize("case,sents,opts", CASES, ids=[_tag(c) for c in CASES])
