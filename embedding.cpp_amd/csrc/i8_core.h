@@ -531,7 +531,7 @@ struct I8ResRing {
     }
 };
 
-template <int WT, int BM, int F, int T, int AH>
+template <int WT, int BM, int F, int T, int AH, bool PIPE = true>
 __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
                                                      float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn) {
     constexpr bool Q1 = wt_q41(WT);
@@ -574,13 +574,13 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
             if (b < 4 * nch) ring.wload(g, (j + A) & 3, ft0, b);
             else if (ftn >= 0) ring.wload(g, (j + A) & 3, ftn, b - 4 * nch);
         };
-        i8_block<WT, BM, F, T, 0, true>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
+        i8_block<WT, BM, F, T, 0, PIPE>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
         refill(0);
-        i8_block<WT, BM, F, T, 1, true>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
+        i8_block<WT, BM, F, T, 1, PIPE>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
         refill(1);
-        i8_block<WT, BM, F, T, 2, true>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
+        i8_block<WT, BM, F, T, 2, PIPE>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
         refill(2);
-        i8_block<WT, BM, F, T, 3, true>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
+        i8_block<WT, BM, F, T, 3, PIPE>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
         refill(3);
     }
 }

@@ -48,6 +48,9 @@ def main():
     assert f(ctypes.c_void_p(0), 0) == 0
     # blocks >= 512 only: the persistent GEMMs (<= 256 workgroups) stamp the same buffer
     h = buf.cpu().numpy().astype(np.uint64).reshape(B, STAMP_TILES, 2, 16)[512:]
+    # STAMP_SLOTS="0,3,4,1,2": the slots in program order (default 0 .. len(names) - 1)
+    order = [int(x) for x in os.environ.get("STAMP_SLOTS", "").split(",") if x] or list(range(len(names)))
+    h = h[:, :, :, order + [k for k in range(16) if k not in order]]
     ns = len(names)
     for w in (0, 1):
         out, tot = [], 0.0
