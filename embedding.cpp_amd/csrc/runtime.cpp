@@ -299,6 +299,12 @@ struct bert_ctx {
     // n_embd 384, head dim 32, int8 QKV): each head's QKV and attention in one
     // kernel (kernels.hip qkv_attention_small_kernel; bitwise the unfused pair)
     bool small_qkva = true;
+    // load-time: the word-embedding table stays in its GGUF row format on the
+    // device (Q4 rows dequantised in embed_ln_kernel as get_rows does, the same
+    // f32 values as the load-time f32 copy; option emb_raw, default 1) instead
+    // of f32 rows: MiniLM Q4_0's table 47 -> 6.6 MB, embed_ln 96-98 -> 90-92 us
+    // on the headline batch (round 6, profiles/r06_embraw_ab.txt), bitwise equal
+    bool emb_raw = true;
     uint64_t opt_gen = 0;  // bumped by every option change (captured graphs are dropped)
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
@@ -900,6 +906,7 @@ EmbedArgs embed_args(const bert_ctx *ctx, Replica &R, const Workspace &w, const 
     ea.pos = R.pos;
     ea.type = R.type;
     ea.word_t = ea.pos_t = ea.type_t = W_F32;  // the replica holds f32 copies (table_f32)
+    if (ctx->emb_raw) ea.word_t = (int)ctx->word_t;  // ... or the word table's own rows (emb_raw)
     ea.ln_w = R.ln_e_w;
     ea.ln_b = R.ln_e_b;
     ea.eps = hp.eps;
@@ -1151,7 +1158,11 @@ bool build_replica(bert_ctx *ctx, const HostModel &hm, Stager &S, Replica &R) {
             b.own.assign((const uint8_t *)v.data(), (const uint8_t *)(v.data() + v.size()));
         });
     };
-    if (!table(&R.word, hm.word) || !table(&R.pos, hm.pos) || !table(&R.type, hm.type) ||
+    auto word_table = [&]() {
+        if (!ctx->emb_raw) return table(&R.word, hm.word);
+        return S.put_ext(&R.word, hm.word->data, hm.word->nbytes);
+    };
+    if (!word_table() || !table(&R.pos, hm.pos) || !table(&R.type, hm.type) ||
         !S.put_ext(&R.ln_e_w, hm.ln_e_w->data, hm.ln_e_w->nbytes) ||
         !S.put_ext(&R.ln_e_b, hm.ln_e_b->data, hm.ln_e_b->nbytes) ||
         !S.put_ext(&R.gelu_tab, tables().gelu.data(), 65536 * 2) ||
@@ -1310,7 +1321,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
     static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows", "graph_seqs",
-                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows"};
+                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows", "emb_raw"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
         std::string env = "BERT_AMD_" + std::string(k);
@@ -1350,6 +1361,12 @@ bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
                 return false;
             }
             ctx->qkva_ntw = (int)v;
+        } else if (p.first == "emb_raw") {
+            if (v < 0 || v > 1) {
+                set_err("bert_amd option emb_raw: must be 0 or 1");
+                return false;
+            }
+            ctx->emb_raw = v != 0;
         } else if (p.first == "q41bf") {
             if (v < -1 || v > 1) {
                 set_err("bert_amd option q41bf: must be -1 (auto), 0 or 1");
@@ -2341,7 +2358,7 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
-        {"q41bf", ctx->q41bf},
+        {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw},
         // resolved: FFN-up / FFN-down on the bf16 scale products (Q4_1 on the int8 GEMMs)
         {"q41bf_up", ctx->wtype == W_Q4_1 && ctx->i8_up && q41bf_for(ctx->q41bf, EPI_GELU_ACT)},
         {"q41bf_down", ctx->wtype == W_Q4_1 && ctx->i8_down &&

@@ -45,6 +45,9 @@ BERT_API struct bert_ctx *bert_amd_load(const char *fname, const int32_t *device
                 (kernels.h W_Q4_1B) instead of the f32 MFMA: 1 every int8
                 projection, 0 none, -1 (default) all but the 384-wide FFN-down
                 + LayerNorm kernel (where they cost more than they save)
+     "emb_raw"  1 (default): the word-embedding table stays in its GGUF row
+                format on the device (dequantised in the embedding kernel as
+                ggml's get_rows does); 0: an f32 copy.  Same results
    and every bert_amd_set_option key below.  Returns NULL on error (an unknown
    key or a bad value included). */
 BERT_API struct bert_ctx *bert_amd_load_opts(const char *fname, const int32_t *devices, int32_t n_devices,

@@ -1,6 +1,6 @@
 """Bitwise comparison of library builds (development A/B on the GPU box).
 
-    python3 tools/bitwise_libs.py lib_a.so lib_b.so ...
+    python3 tools/bitwise_libs.py lib_a.so lib_b.so[@BERT_AMD_KEY=VALUE,...] ...
 
 Each library runs in its own process (BERT_AMD_LIB) on the same synthetic
 MiniLM Q4_0 / Q4_1 models and the same batches (the headline shape, a ragged
@@ -30,7 +30,7 @@ def child(out):
         "one": [[101] + rng.integers(1000, 30522, 14).tolist() + [102]],
     }
     res = {}
-    for ft in ("q4_0", "q4_1"):
+    for ft in os.environ.get("BITWISE_FTYPES", "q4_0,q4_1").split(","):
         path = os.path.join(d, f"bitwise_minilm_{ft}.gguf")
         if not os.path.exists(path):
             bertlib.synth_model(path, "minilm", ft, seed=20250117, w_std=0.05)
@@ -44,9 +44,12 @@ def child(out):
 def main():
     libs = sys.argv[1:]
     outs = []
-    for i, lib in enumerate(libs):
+    for i, spec in enumerate(libs):
+        # "lib.so" or "lib.so@KEY=VALUE,KEY=VALUE": environment options for that run
+        lib, _, envs = spec.partition("@")
         out = f"/tmp/bitwise_{i}.npz"
         env = dict(os.environ, BERT_AMD_LIB=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in envs.split(",") if kv)
         subprocess.run([sys.executable, __file__, "--child", out], env=env, check=True, timeout=300)
         outs.append(np.load(out))
     ok = True
