@@ -28,6 +28,7 @@ def child(out):
         "fixed": [[101] + rng.integers(1000, 30522, 126).tolist() + [102] for _ in range(512)],
         "ragged": [[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in rng.integers(8, 129, 400)],
         "one": [[101] + rng.integers(1000, 30522, 14).tolist() + [102]],
+        "few": [[101] + rng.integers(1000, 30522, n - 2).tolist() + [102] for n in (5, 40, 77, 128)],
     }
     res = {}
     for ft in os.environ.get("BITWISE_FTYPES", "q4_0,q4_1").split(","):
