@@ -1026,8 +1026,12 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
             }
             if (!force_pack && !qkv_attention_pack_pays(G[gi].nseq, ntl[gi])) ntl[gi] = G[gi].nseq;  // plain kernel
         }
-        // pageable source: the copy is staged before the call returns, so ht may be reused
-        HIP_OK(hipMemcpyAsync(w.tiles, ht.data(), (size_t)2 * n_seqs * 4, hipMemcpyHostToDevice, st));
+        // pageable source: the copy is staged before the call returns, so ht may be reused.
+        // Only packed groups read the table (run_layer: tiles = nullptr when every
+        // tile is one sentence), so a batch with none skips the upload
+        bool packs = false;
+        for (int gi = 0; gi < ng; gi++) packs |= ntl[gi] < G[gi].nseq;
+        if (packs) HIP_OK(hipMemcpyAsync(w.tiles, ht.data(), (size_t)2 * n_seqs * 4, hipMemcpyHostToDevice, st));
         if (ng == 2) {
             HIP_OK(hipEventRecord(ln.ev_fork, st));
             HIP_OK(hipStreamWaitEvent(ln.stream2, ln.ev_fork, 0));
