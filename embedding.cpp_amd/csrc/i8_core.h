@@ -15,15 +15,6 @@ namespace bertamd {
 #ifndef I8_Q41_GENERIC
 #define I8_Q41_GENERIC 0
 #endif
-// Block fold form (A/B; every form gives the same bits): 0 = v_cvt_f32_i32 +
-// v_fma_f32 per output; 1 = the isum MFMA accumulates onto the bit pattern of
-// 1.5 * 2^23 (srcC = 0x4B400000), so each output already reads as the float
-// 1.5 * 2^23 + isum (exact: |isum| <= 32 * 127 * 15 < 2^22), then v_sub_f32
-// (exact) + v_fma_f32; 2 = as 1 with the subtraction and the fma on output
-// pairs (v_pk_add_f32 + v_pk_fma_f32: 16 instead of 32 per tile and block).
-#ifndef I8_FOLD
-#define I8_FOLD 0
-#endif
 // W_Q4_1B (kernels.h): Q4_1's scale products on the bf16 MFMA — d_w * d_a and
 // m_w * s_a (fp16 x f32) as sums of exact bf16 x bf16 partial products (d_w =
 // w0 + w1, d_a = a0 + a1 + a2 in bf16 parts) in one v_mfma_f32_32x32x16_bf16
@@ -323,40 +314,24 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
     // (PIPE false: issue and fold tile by tile; latency left to other waves)
     int16v is[2];
     float16v dd[2];
-    constexpr bool MAGIC = I8_FOLD != 0 && !I8_Q41_GENERIC;
-    int16v c0 = __builtin_bit_cast(int16v, zf);
-    if constexpr (MAGIC) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) c0[i] = 0x4B400000;
-    }
-    is[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[0], cur.xa[0], c0, 0, 0, 0);
+    is[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[0], cur.xa[0], __builtin_bit_cast(int16v, zf), 0, 0, 0);
     dd[0] = ddmfma(0, 0);
 #pragma unroll
     for (int p = 0; p < F * T; p++) {
         if (!PIPE && p > 0) {
-            is[p & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[p / T], cur.xa[p % T], c0, 0, 0, 0);
+            is[p & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[p / T], cur.xa[p % T], __builtin_bit_cast(int16v, zf),
+                                                              0, 0, 0);
             dd[p & 1] = ddmfma(p / T, p % T);
         }
         if (PIPE && p + 1 < F * T) {
-            is[(p + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[(p + 1) / T], cur.xa[(p + 1) % T], c0, 0, 0, 0);
+            is[(p + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wfc[(p + 1) / T], cur.xa[(p + 1) % T],
+                                                                     __builtin_bit_cast(int16v, zf), 0, 0, 0);
             dd[(p + 1) & 1] = ddmfma((p + 1) / T, (p + 1) % T);
         }
         // tile p + 1's MFMAs are issued before tile p's fold reads tile p's
         // results (left to itself the scheduler folds right behind the MFMA
         // that produces the operands and waits out its latency)
         __builtin_amdgcn_sched_barrier(0);
-#if I8_FOLD == 2 && !I8_Q41_GENERIC
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-            float2v x = {__int_as_float(is[p & 1][i]), __int_as_float(is[p & 1][i + 1])};
-            x = x - float2v{12582912.0f, 12582912.0f};  // exact: (float) isum
-            float2v v = __builtin_elementwise_fma(x, float2v{dd[p & 1][i], dd[p & 1][i + 1]},
-                                                  float2v{acc[p / T][p % T][i], acc[p / T][p % T][i + 1]});
-            asm volatile("" : "+v"(v));
-            acc[p / T][p % T][i] = v[0];
-            acc[p / T][p % T][i + 1] = v[1];
-        }
-#else
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             // (one v_fma_f32 per output: the packed v_pk_fma_f32 fold measured slower
@@ -368,13 +343,11 @@ __device__ __forceinline__ void i8_block(const char *buf, int tt0, const int4v (
             else
                 v = __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], acc[p / T][p % T][i]);
 #else
-            const float x = MAGIC ? __int_as_float(is[p & 1][i]) - 12582912.0f : (float)is[p & 1][i];
-            float v = __builtin_fmaf(x, dd[p & 1][i], acc[p / T][p % T][i]);
+            float v = __builtin_fmaf((float)is[p & 1][i], dd[p & 1][i], acc[p / T][p % T][i]);
 #endif
             asm volatile("" : "+v"(v));  // keep the fold here: sunk past the MFMAs it would keep every tile live
             acc[p / T][p % T][i] = v;
         }
-#endif
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -531,7 +504,7 @@ struct I8ResRing {
     }
 };
 
-template <int WT, int BM, int F, int T, int AH, bool PIPE = true>
+template <int WT, int BM, int F, int T, int AH>
 __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
                                                      float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn) {
     constexpr bool Q1 = wt_q41(WT);
@@ -574,13 +547,13 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
             if (b < 4 * nch) ring.wload(g, (j + A) & 3, ft0, b);
             else if (ftn >= 0) ring.wload(g, (j + A) & 3, ftn, b - 4 * nch);
         };
-        i8_block<WT, BM, F, T, 0, PIPE>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
+        i8_block<WT, BM, F, T, 0, true>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
         refill(0);
-        i8_block<WT, BM, F, T, 1, PIPE>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
+        i8_block<WT, BM, F, T, 1, true>(buf, tt0, ring.wf[1], ws, wd, wm, a1, a0, acc);
         refill(1);
-        i8_block<WT, BM, F, T, 2, PIPE>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
+        i8_block<WT, BM, F, T, 2, true>(buf, tt0, ring.wf[2], ws, wd, wm, a0, a1, acc);
         refill(2);
-        i8_block<WT, BM, F, T, 3, PIPE>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
+        i8_block<WT, BM, F, T, 3, true>(buf, tt0, ring.wf[3], ws, wd, wm, a1, a0, acc);
         refill(3);
     }
 }

@@ -1724,39 +1724,17 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 // p - 1's attention; two barriers per period (the consumers are done with the
 // tiles; the tiles hold the next head).  LDS: the panel (58 KB), one head's
 // tiles (57 KB), the exp table (40 KB).
-//
-// Consumer pairs (QKPC_PAIRS, unpacked tiles): 8 consumer waves, two per query
-// block.  Wave A scores key tiles 0-1, wave B key tiles 2-3; they exchange
-// their row maxima through LDS (ggml's max is exact in any order), each turns
-// its tiles into the table's probabilities and exact integer sums; A runs the
-// V.P chain over tiles 0-1 and hands its accumulator to B through the query
-// block's own Q rows (free once both waves hold their Q fragments), and B
-// continues the same chain over tiles 2-3 and stores the context — the single
-// consumer's MFMA chain in the same order, so the results are bitwise the
-// 4-consumer form's (and the unfused pair's).  Pair hand-offs are LDS words
-// with bounded spins.
-#ifndef QKPC_PAIRS
-#define QKPC_PAIRS 0  // round 6 A/B (§8 "Consumer pairs"); off: measured slower with the LDS exp table
-#endif
-constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves (packed tiles / no pairs)
-__host__ __device__ constexpr int qkpc_nw(bool pk) { return (QKPC_PAIRS && !pk) ? QKPC_NP + 8 : QKPC_NW; }
+constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
 #ifndef QKPC_CPRIO
 #define QKPC_CPRIO 0  // A/B: static issue priority of the consumer waves (round 4: 0, 1 and 2 within noise)
-#endif
-#ifndef QKPC_EXPREG
-#define QKPC_EXPREG 0  // A/B: soft_max's exp in registers (v_exp_f32), not the LDS table (tools/exp_probe.hip)
-#endif
-#ifndef QKPC_PPIPE
-#define QKPC_PPIPE 0  // consumer pairs: the producers' two-tile MFMA pipeline (i8_block PIPE; 32 VGPRs)
 #endif
 #ifndef QKPC_AHEAD
 #define QKPC_AHEAD 2  // the producers' weight blocks in flight (i8_core.h I8ResRing)
 #endif
 
 template <bool PK>
-__global__ __launch_bounds__(qkpc_nw(PK) * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
-    constexpr int WT = W_Q4_0, D = 32, NP = QKPC_NP, NW = qkpc_nw(PK), BM = 128, NT = NW * 64;
-    constexpr bool PAIRS = NW > QKPC_NW;
+__global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
+    constexpr int WT = W_Q4_0, D = 32, NP = QKPC_NP, NW = QKPC_NW, BM = 128, NT = NW * 64;
     constexpr int NK = 128, KST = D + 8, VST = NK + 4, E = 384, NKB = E / 32;
     using C = I8Chunk<BM, false>;
     constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
@@ -1765,17 +1743,10 @@ __global__ __launch_bounds__(qkpc_nw(PK) * 64) void qkv_attention_pc_kernel(Gemm
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     __shared__ int qtab[PK ? 4 : 1][4];     // query block -> {first tile row of its sentence, length, first query, vs}
     __shared__ uint8_t vslot[PK ? NK : 1];  // tile row -> V^T key slot
-    // consumer pairs: row maxima [pair][half][query], hand-off sequence words [pair][2]
-    __shared__ float pmx[PAIRS ? 4 : 1][2][32];
-    __shared__ int pseq[PAIRS ? 4 : 1][2][2];
-    __shared__ __attribute__((aligned(16))) float sbias[PAIRS ? 3 * E : 1];  // pairs: the QKV bias (registers are short)
     const int s0 = PK ? a.tiles[2 * blockIdx.x] : (int)blockIdx.x;
     const int ns = PK ? a.tiles[2 * blockIdx.x + 1] : 1;
     const int beg = a.offsets[s0], n = a.offsets[s0 + ns] - beg;
     if (n > NK || n <= 0 || ns > 4 || g.K != E || a.E != E) return;
-    if (PAIRS && threadIdx.x < 16) (&pseq[0][0][0])[threadIdx.x] = -1;
-    if constexpr (PAIRS)
-        for (int i = threadIdx.x; i < 3 * E / 4; i += NT) ((float4v *)sbias)[i] = ((const float4v *)g.bias)[i];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the role branches are scalar
     const int r = lane & 31, hh = lane >> 5;
@@ -1835,28 +1806,17 @@ __global__ __launch_bounds__(qkpc_nw(PK) * 64) void qkv_attention_pc_kernel(Gemm
             const int f0 = p * 3 * D + part * D + 16 * hh;  // head-major feature of acc[..][0]
             float bias[16];
             if (p < H) {
-                if constexpr (!PAIRS) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
+                for (int q = 0; q < 4; q++) {
+                    const float4v b4 = *(const float4v *)(g.bias + f0 + 4 * q);
 #pragma unroll
-                        for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
-                    }
+                    for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
                 }
-                i8_resident_mainloop<WT, BM, 1, 2, QKPC_AHEAD, QKPC_PPIPE || !PAIRS>(g, apanel, 3 * p + part, tt0, acc, ring,
-                                                                                    p + 1 < H ? 3 * (p + 1) + part : -1);
+                i8_resident_mainloop<WT, BM, 1, 2>(g, apanel, 3 * p + part, tt0, acc, ring, p + 1 < H ? 3 * (p + 1) + part : -1);
             }
             STAMP(p, 1, NW);
             __syncthreads();  // X: the consumers are done with head p - 1's tiles
             if (p < H) {
-                if constexpr (PAIRS) {
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const float4v b4 = *(const float4v *)(sbias + f0 + 4 * q);
-#pragma unroll
-                        for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
-                    }
-                }
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
                     const int row = 32 * (tt0 + t) + r;  // tile row (token of the tile)
@@ -1889,127 +1849,6 @@ __global__ __launch_bounds__(qkpc_nw(PK) * 64) void qkv_attention_pc_kernel(Gemm
             }
             STAMP(p, 2, NW);
             __syncthreads();  // Y: head p's tiles are complete
-            STAMP(p + 1, 0, NW);
-        }
-    } else if constexpr (PAIRS) {
-        // ---- consumer pair: query block qb of head p - 1, key tiles 2 hf .. 2 hf + 1
-        const int qb = (wv - NP) >> 1, hf = (wv - NP) & 1;
-        const _Float16 *Qh = plane(0), *Ql = plane(1), *Kh = plane(2), *Kl = plane(3), *Vh = plane(4), *Vl = plane(5);
-        const int qrel = 32 * qb;
-        const bool qact = qrel < n;
-        const int qrow = qrel + r;  // rows past the sentence read finite LDS data; never stored
-        // the hand-off buffer: this query block's own Q rows (32 x KST halves in each of
-        // Qh / Ql), free once both waves of the pair have read their Q fragments
-        float *hand_hi = (float *)(tiles + (size_t)qrel * KST * 2);
-        float *hand_lo = (float *)(tiles + NK * KST * 2 + (size_t)qrel * KST * 2);
-        // bounded LDS spin on the partner's sequence word (gives up after ~1 s: never a hang)
-        auto wait_seq = [&](int slot, int want) {
-            for (int it = 0; it < (1 << 22); it++) {
-                if (__hip_atomic_load(&pseq[qb][slot][1 - hf], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == want)
-                    break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        };
-        auto post_seq = [&](int slot, int v) {
-            __hip_atomic_store(&pseq[qb][slot][hf], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        };
-        for (int p = 0; p <= H; p++) {
-            const int head = p - 1;
-            const bool act = head >= 0 && qact;
-            float16v o[1];
-            uint32_t sum = 0;
-            if (act) {
-                const int nkt = (n + 31) >> 5;
-                int klim = n - 4 * hh;  // key 32 kt + (j & 3) + 8 (j >> 2) + 4 hh valid while < n (opaque per head)
-                asm volatile("" : "+v"(klim));
-                half8 qh[D / 16], ql[D / 16];
-#pragma unroll
-                for (int ks = 0; ks < D / 16; ks++) {
-                    qh[ks] = *(const half8 *)(Qh + qrow * KST + 16 * ks + 8 * hh);
-                    ql[ks] = *(const half8 *)(Ql + qrow * KST + 16 * ks + 8 * hh);
-                }
-                float16v Sk[2];
-                float mx = -INFINITY;
-#pragma unroll
-                for (int j2 = 0; j2 < 2; j2++) {
-                    const int kt = 2 * hf + j2;
-                    if (kt < nkt) {
-                        float16v S = attn_qk<D>(Kh, Kl, KST, 32 * kt, r, hh, qh, ql);
-                        if (32 * kt + 32 > n) {
-#pragma unroll
-                            for (int j = 0; j < 16; j++)
-                                if (32 * kt + (j & 3) + 8 * (j >> 2) >= klim) S[j] = -INFINITY;
-                        }
-                        Sk[j2] = S;
-#pragma unroll
-                        for (int j = 0; j < 16; j++) mx = fmaxf(mx, S[j]);
-                    }
-                }
-                mx = fmaxf(mx, __shfl_xor(mx, 32));
-                // exchange the row maxima (after this both waves have read their Q rows)
-                if (hh == 0) pmx[qb][hf][r] = mx;
-                post_seq(0, p);
-                wait_seq(0, p);
-                STAMP(p, 3, NW);
-                mx = fmaxf(mx, pmx[qb][1 - hf][r]) * a.scale;
-                const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
-                half8 ph[2][2];
-#pragma unroll
-                for (int j2 = 0; j2 < 2; j2++) {
-                    const int kt = 2 * hf + j2;
-                    if (kt >= nkt) continue;
-#pragma unroll
-                    for (int j = 0; j < 16; j += 2) {
-                        const float2v d2 = mx2 - float2v{Sk[j2][j], Sk[j2][j + 1]} * sc2;
-                        uint16_t pb[2];
-#pragma unroll
-                        for (int e = 0; e < 2; e++) {
-                            const uint32_t hm = f2h(d2[e]);
-                            pb[e] = QKPC_EXPREG ? (uint16_t)f2h(__expf(-h2f((uint16_t)hm)))
-                                                : etab[epos + min(hm, (uint32_t)eneg)];
-                            ph[j2][(j + e) >> 3][(j + e) & 7] = __builtin_bit_cast(_Float16, pb[e]);
-                        }
-                        const float2v pp = float2v{h2f(pb[0]), h2f(pb[1])} * float2v{16777216.0f, 16777216.0f};
-                        sum += (uint32_t)pp[0] + (uint32_t)pp[1];
-                    }
-                }
-                o[0] = float16v{};
-                STAMP(p, 4, NW);
-                if (hf == 1) {  // continue A's V.P chain: its accumulator and sum
-                    wait_seq(1, p);
-                    STAMP(p, 5, NW);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        o[0][i] = hand_hi[i * 64 + lane];
-                        o[0][i + 8] = hand_lo[i * 64 + lane];
-                    }
-                    sum += ((const uint32_t *)hand_hi)[8 * 64 + lane];
-                }
-#pragma unroll
-                for (int j2 = 0; j2 < 2; j2++) {
-                    const int kt = 2 * hf + j2;
-                    if (kt < nkt) attn_pv_h<D, 1>(o, Vh, Vl, VST, 32 * kt, r, hh, ph[j2], 0);
-                }
-                if (hf == 0) {  // hand the chain to B
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        hand_hi[i * 64 + lane] = o[0][i];
-                        hand_lo[i * 64 + lane] = o[0][i + 8];
-                    }
-                    ((uint32_t *)hand_hi)[8 * 64 + lane] = sum;
-                    post_seq(1, p);
-                }
-            }
-            STAMP(p, 1, NW);
-            __syncthreads();  // X: this head's tiles may be overwritten
-            if (act && hf == 1) {
-                sum += __shfl_xor(sum, 32);
-                int orow = beg + qrow;
-                asm volatile("" : "+v"(orow));
-                attn_store_ctx<WT, D, 1>(a, o, (float)(1.0 / ((double)sum * 0x1p-24)), orow, qrow < n, head, hh, 0);
-            }
-            STAMP(p, 2, NW);
-            __syncthreads();  // Y
             STAMP(p + 1, 0, NW);
         }
     } else {
@@ -2119,9 +1958,9 @@ static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks,
     if constexpr (D == 32 && WT == W_Q4_0) {
         if (ntw == 0) {  // producer / consumer waves (qkv_attention_pc_kernel; g.Wi: int8 QKV weights)
             if (pk)
-                hipLaunchKernelGGL((qkv_attention_pc_kernel<true>), dim3(n_blocks), dim3(qkpc_nw(true) * 64), 0, s, g, a);
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<true>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a);
             else
-                hipLaunchKernelGGL((qkv_attention_pc_kernel<false>), dim3(n_blocks), dim3(qkpc_nw(false) * 64), 0, s, g, a);
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<false>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a);
             return hipGetLastError();
         }
     }

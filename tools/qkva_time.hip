@@ -149,7 +149,7 @@ int main(int argc, char **argv) {
         g.K = K;
         auto launch = [&] {
             if (pc)
-                hipLaunchKernelGGL((qkv_attention_pc_kernel<false>), dim3(S), dim3(qkpc_nw(false) * 64), 0, 0, g, a);
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<false>), dim3(S), dim3(QKPC_NW * 64), 0, 0, g, a);
             else
                 hipLaunchKernelGGL((qkv_attention_kernel<W_Q4_0, 32, 2, false>), dim3(S), dim3(QKVA_NW * 64), 0, 0, g, a);
         };
