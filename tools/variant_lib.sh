@@ -1,12 +1,12 @@
 #!/bin/bash
 # Build a variant of build/libbert.so with extra compile flags on the HIP
 # sources (development A/B; run here, not on the GPU box):
-#   tools/variant_lib.sh <name> "<extra hipcc flags>"  ->  build/var/<name>/libbert.so
+#   tools/variant_lib.sh <name> "<extra hipcc flags>"  ->  build/ab/<name>/libbert.so (delete after the A/B; build/var is kept off GPU pushes)
 set -e
 cd "$(dirname "$0")/.."
 make -s build/libbert.so
 NAME=$1; FLAGS=$2
-OUT=build/var/$NAME
+OUT=build/ab/$NAME
 mkdir -p "$OUT"
 HIPFLAGS="-O3 -std=c++17 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-unused-value -Wno-unused-result -fPIC -fvisibility=hidden -ffp-contract=off --offload-arch=gfx950 -Iinclude -Iembedding.cpp_amd/csrc"
 for f in kernels gemm_i8; do
