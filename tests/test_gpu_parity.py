@@ -265,6 +265,23 @@ def test_q41bf_default_resolution(model_dir):
     assert m0.get_option("q41bf_up") == 0 and m0.get_option("q41bf_down") == 0
 
 
+@pytest.mark.parametrize("ftype", ["f16", "q4_0", "q4_1"])
+def test_word_table_forms_bitwise(ftype, model_dir):
+    """Load option emb_raw: the word-embedding table kept in its GGUF row form
+    (dequantised in embed_ln_kernel as ggml's get_rows does; the default) and
+    as an f32 copy give the same embeddings bit for bit, on a ragged batch and
+    one sentence."""
+    p, m = get_model(model_dir, "minilm", ftype)
+    m32 = bertlib.BertModel(p, options={"emb_raw": 0})
+    try:
+        assert m.get_option("emb_raw") == 1 and m32.get_option("emb_raw") == 0
+        toks = [sentence(1200 + i, n, 30522) for i, n in enumerate([1, 7, 64, 128, 33, 100] * 9)]
+        assert np.array_equal(m.eval_batch(toks), m32.eval_batch(toks))
+        assert np.array_equal(m.eval(toks[3]), m32.eval(toks[3]))
+    finally:
+        m32.close()
+
+
 def test_bf16_split_scale_product_probe():
     """tools/mfma_bf16_split_probe.hip: how v_mfma_f32_32x32x16_bf16 rounds a
     sum of six exact bf16 partial products (the q41bf scale products) against
