@@ -325,6 +325,27 @@ def test_full_size_north_star_batch(model_dir):
     assert cos(out[:4], fx_emb).min() >= COS_TOL
 
 
+@pytest.mark.parametrize("case,B,N", [("c4_e5_f16", 512, 256), ("c5_bge_q4_1", 1024, 512)])
+def test_full_size_config_batches(case, B, N, model_dir):
+    """BASELINE configs 4 and 5 at their full per-GPU size (e5-base f16 512 x 256,
+    bge-large Q4_1 1024 x 512, 24 layers): size-independent properties on
+    every row — finite, unit norm, run-to-run bitwise, a sentence alone equal
+    to its row — and the golden fixture (its sentences are this batch's first
+    rows) within the parity bound."""
+    meta, toks, want = load_case(case)
+    p, m = get_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
+    full = [sentence(i, N, meta["hparams"]["n_vocab"]) for i in range(B)]
+    assert full[:len(toks)] == [list(t) for t in toks]
+    out = m.eval_batch(full)
+    assert np.all(np.isfinite(out))
+    assert np.allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)
+    assert np.array_equal(out, m.eval_batch(full))
+    assert np.array_equal(m.eval(full[B // 2 + 3]), out[B // 2 + 3])
+    c = cos(out[:len(toks)], want)
+    print(f"{case} full size: fixture rows 1-cos {1 - c}")
+    assert np.all(1 - c <= parity_bound(meta)), (1 - c, parity_bound(meta))
+
+
 class Hip:
     """The HIP runtime libbert.so itself links (/opt/rocm libamdhip64.so.7),
     through ctypes: device buffers and streams for the device-resident API
