@@ -52,7 +52,7 @@ def max_ulp(a, b):
 
 # (case, sentences of the fixture to use, load options): C3 on the fused QKV +
 # attention kernel (fuse_min 0: a 4-sentence batch would otherwise take the
-# unfused pair), C2 F16, and the 24-layer C5 whose 1 - cos 1.75e-3 this explains
+# unfused pair), C2 F16, and the 24-layer C5 whose 1 - cos ~2e-3 this explains
 CASES = [
     ("c5_bge_q4_1", [0], {"i8": "all"}),
     ("c3_minilm_q4_0", [0, 1], {"fuse_min": 0}),
