@@ -208,7 +208,7 @@ def dtype_note(ftype: str, arith: dict) -> str:
         s = "Q4 x Q8 as ggml vec_dot_q4_x_q8_x: "
         if i8:
             s += f"{'/'.join(i8)} on int8 MFMA (exact block isum, per-block d_w*d_a fold in f32)"
-            bf = [k for k in ("up", "down") if arith.get(f"q41bf_{k}")]
+            bf = [k for k in ("qkv", "o", "up", "down") if arith.get(f"q41bf_{k}")]
             if bf:
                 s += f" ({'/'.join(bf)}: Q4_1 scale products as exact bf16 partial products on the bf16 MFMA)"
         if f16:
@@ -469,8 +469,8 @@ def main():
     prof = model.profile_read()
     model.profile(False)
     model.set_option("split", int(os.environ.get("BERT_AMD_SPLIT", "1")[:1] != "0"))
-    arith = {k: model.get_option(k) for k in ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf_up",
-                                              "q41bf_down")}
+    arith = {k: model.get_option(k) for k in ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf_qkv",
+                                              "q41bf_o", "q41bf_up", "q41bf_down")}
     kern = {}
     for name, (ms, cnt) in prof.items():
         parts = kernel_parts(name, B, N, hp, arith, args.ftype)

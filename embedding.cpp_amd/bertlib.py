@@ -304,7 +304,8 @@ class BertModel:
 
     def get_option(self, key: str) -> int:
         """bert_amd_get_option: a pipeline option, or a resolved load-time choice
-        ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf_up", "q41bf_down")."""
+        ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf", "q41bf_qkv",
+        "q41bf_o", "q41bf_up", "q41bf_down", "emb_raw")."""
         v = ctypes.c_int32(0)
         if self.lib.bert_amd_get_option(self.ctx, key.encode(), ctypes.byref(v)) != 0:
             raise ValueError(f"bert_amd_get_option({key}) failed: {last_error()}")

@@ -2364,6 +2364,8 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
         {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw},
         // resolved: FFN-up / FFN-down on the bf16 scale products (Q4_1 on the int8 GEMMs)
+        {"q41bf_qkv", ctx->wtype == W_Q4_1 && ctx->i8_qkv && q41bf_for(ctx->q41bf, EPI_QKV)},
+        {"q41bf_o", ctx->wtype == W_Q4_1 && ctx->i8_o && q41bf_for(ctx->q41bf, ctx->hp.n_embd == 384 ? EPI_LN : EPI_RESID)},
         {"q41bf_up", ctx->wtype == W_Q4_1 && ctx->i8_up && q41bf_for(ctx->q41bf, EPI_GELU_ACT)},
         {"q41bf_down", ctx->wtype == W_Q4_1 && ctx->i8_down &&
                            q41bf_for(ctx->q41bf, ctx->hp.n_embd == 384 ? EPI_LN : EPI_RESID)}};

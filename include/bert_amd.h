@@ -160,8 +160,9 @@ BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int3
    "i8_qkv", "i8_up", "i8_o", "i8_down" (1 when that Q4 projection runs on
    the int8-MFMA GEMMs: for QKV, the producer / consumer kernel's int8 copy
    and its unfused int8 twin), "q41bf" (the load option: -1 auto, 0, 1) and
-   "q41bf_up", "q41bf_down" (1 when that Q4_1 projection's scale products
-   run on the bf16 MFMA, W_Q4_1B).  Lets bench.py price each kernel on the
+   "q41bf_qkv", "q41bf_o", "q41bf_up", "q41bf_down" (1 when that Q4_1
+   projection's int8 GEMM takes its scale products on the bf16 MFMA,
+   W_Q4_1B).  Lets bench.py price each kernel on the
    arithmetic it runs.  Returns 0, or -2 on an unknown key. */
 BERT_API int32_t bert_amd_get_option(struct bert_ctx *ctx, const char *key, int32_t *value);
 

@@ -262,8 +262,17 @@ def test_q41bf_default_resolution(model_dir):
     p, m = get_model(model_dir, "minilm", "q4_1")
     assert m.get_option("q41bf") == -1
     assert m.get_option("q41bf_up") == 1 and m.get_option("q41bf_down") == 0
+    assert m.get_option("q41bf_qkv") == 0 and m.get_option("q41bf_o") == 0  # split-fp16 by default
     p0, m0 = get_model(model_dir, "minilm", "q4_0")
-    assert m0.get_option("q41bf_up") == 0 and m0.get_option("q41bf_down") == 0
+    for k in ("qkv", "o", "up", "down"):
+        assert m0.get_option(f"q41bf_{k}") == 0
+    # every projection on the int8 GEMMs: QKV (EPI_QKV) takes the bf16 products,
+    # the 384-wide O + LN kernel does not
+    ma = bertlib.BertModel(p, options={"i8": "all"})
+    try:
+        assert [ma.get_option(f"q41bf_{k}") for k in ("qkv", "o", "up", "down")] == [1, 0, 1, 0]
+    finally:
+        ma.close()
 
 
 @pytest.mark.parametrize("ftype", ["f16", "q4_0", "q4_1"])
