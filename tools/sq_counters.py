@@ -85,7 +85,7 @@ def main(cyc_dir, ins_dir, stats_csv, out, source):
             "valu_issue_frac_of_wall": round(2 * c["SQ_INSTS_VALU"] / (1024 * cyc), 3),
             "mfma_busy_frac_of_wall": round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc), 3),
         }
-    doc = {"source": source + "; " + __doc__.split("\n\n")[1].replace("\n", " ").strip(), "kernels": res}
+    doc = {"source": source + "; " + __doc__.split("\n\n")[2].replace("\n", " ").strip(), "kernels": res}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps(doc, indent=1))
