@@ -129,7 +129,9 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
 // the chunk starts), and the previous tile's LN output leaves xs during the same
 // chunks, each wave draining one 1 KiB piece of xs to X just before refilling
 // that piece with the new residual; the last tile's output leaves after the loop.
-__device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ (r & 15)); }
+// (i8_xs_chunk: i8_core.h.  The LN epilogue below is i8_ln384_epilogue of i8_core.h
+// written out, the same arithmetic in the same order: qkv_attention_pc_kernel's O tail
+// runs that helper and tests/test_gpu_parity.py checks the two bitwise.)
 
 #ifndef I8_LN_OV
 #define I8_LN_OV 1

@@ -448,6 +448,95 @@ __device__ __forceinline__ void i8_store_q8_half(const ActPtr &out, int64_t ld, 
     }
 }
 
+// 16-byte chunk c of row r of a 64-row x 384-feature f32 tile in LDS (the LN
+// kernels' residual tile): chunk c ^ (r & 15), so row-per-lane reads are
+// conflict-free.
+__device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ (r & 15)); }
+
+// The LayerNorm epilogue of a 64-row x 384-feature tile (bert.cpp:944-962 and
+// :973-992): X = LN((b + W.x) + X).  12 waves; wave w holds acc[0][t] = features
+// 32 w + 16 hh .. + 15 of token 32 t + (lane & 31); the residual tile is in xs
+// (i8_xs_chunk layout) and the LN output replaces it there; the Q8 form goes to
+// g.out_act (rows m0 ..).  ggml_norm's double sums go lane -> lane pair -> the
+// twelve waves (red: [2][12][64], fixed order).  Shared by i8_ln384_kernel and
+// the O tail of qkv_attention_pc_kernel, so the two are bitwise equal.  MASK:
+// rows >= nvalid are computed but their Q8 form is not stored.  Starts after a
+// barrier that published xs; contains two barriers; ends after its stores.
+template <int WT, bool MASK>
+__device__ __forceinline__ void i8_ln384_epilogue(float16v (&acc)[1][2], float *xs, double (*red)[12][64],
+                                                  const GemmArgs &g, int64_t m0, int nvalid, int it) {
+    constexpr int T = 2, NCOL = 384, NWV = 12;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l32 = lane & 31, hh = lane >> 5;
+    const int ft0 = wv, col = 32 * ft0 + 16 * hh;
+    // v = (b + W.x) + x  (ggml: add(repeat(b), mul_mat) then add(cur, inpL))
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const int r = 32 * t + l32;
+        double s = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const float4v x4 = *(const float4v *)(xs + 4 * i8_xs_chunk(r, (col >> 2) + qq));
+            const float4v b4 = *(const float4v *)(g.bias + col + 4 * qq);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float v = (b4[j] + acc[0][t][4 * qq + j]) + x4[j];
+                acc[0][t][4 * qq + j] = v;
+                s += (double)v;
+            }
+        }
+        s += __shfl_xor(s, 32);
+        if (hh == 0) red[0][wv][r] = s;
+    }
+    __syncthreads();
+    STAMP(it, 3, NWV);
+    float mean[T];
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const int r = 32 * t + l32;
+        double tot = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWV; w++) tot += red[0][w][r];
+        mean[t] = (float)(tot / NCOL);
+        double s2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const float v = acc[0][t][i] - mean[t];
+            acc[0][t][i] = v;
+            s2 += (double)(v * v);
+        }
+        s2 += __shfl_xor(s2, 32);
+        if (hh == 0) red[1][wv][r] = s2;
+    }
+    __syncthreads();
+    STAMP(it, 4, NWV);
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const int r = 32 * t + l32;
+        const int64_t row = m0 + r;
+        double tot = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWV; w++) tot += red[1][w][r];
+        const float var = (float)(tot / NCOL);
+        const float scale = 1.0f / sqrtf(var + g.eps);
+        float y[16];
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const float4v w4 = *(const float4v *)(g.ln_w + col + 4 * qq);
+            const float4v b4 = *(const float4v *)(g.ln_b + col + 4 * qq);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float z = acc[0][t][4 * qq + j] * scale;
+                z = w4[j] * z;
+                y[4 * qq + j] = z + b4[j];
+            }
+            // in place: each (row, chunk) is this lane's alone
+            *(float4v *)(xs + 4 * i8_xs_chunk(r, (col >> 2) + qq)) =
+                float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
+        }
+        if (!MASK || r < nvalid) i8_store_q8_half<WT>(g.out_act, NCOL, row, ft0, hh, y);
+    }
+}
+
 // XCD-aware tile order (as gemm_kernel): linear ids are dealt round-robin over
 // the 8 XCDs; each XCD walks a contiguous range, n fastest.
 __device__ __forceinline__ int xcd_linear(int orig, int nwg) {
@@ -504,9 +593,12 @@ struct I8ResRing {
     }
 };
 
-template <int WT, int BM, int F, int T, int AH>
+// hook(c, nch) runs at the start of every chunk c (the caller's memory traffic
+// interleaved with the main loop, as in i8_mainloop).
+template <int WT, int BM, int F, int T, int AH, typename Hook = I8NoHook>
 __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
-                                                     float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn) {
+                                                     float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn,
+                                                     const Hook &hook = Hook()) {
     constexpr bool Q1 = wt_q41(WT);
     using C = I8Chunk<BM, Q1, WT == W_Q4_1B>;
     const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -534,6 +626,7 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
         const int b0 = 4 * c;
         const bool last = c + 1 == nch;
         const char *buf = apanel + c * C::BYTES;
+        hook(c, nch);
         wscale_use();
         if (!last) ring.sload(g, ft0, c + 1);
         else if (ftn >= 0) ring.sload(g, ftn, 0);

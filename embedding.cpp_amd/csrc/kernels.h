@@ -164,8 +164,12 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles);
 // of the kernel's QKV weight copy (runtime.cpp), chosen per context at load;
 // 0: the producer / consumer kernel (head dim 32, n_embd 384; plain tile order).
 bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw);
-// n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
-hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s);
+// n_blocks: tiles (a.tiles) or sentences (a.tiles == null).  o (ntw 0 only):
+// the O projection + residual + LayerNorm runs inside the same kernel after the
+// attention (the O tail), with the int8 O weights o->Wi, bitwise the separate
+// i8 EPI_LN launch (launch_gemm_i8) on a.ctx; o->X / o->out_act: workspace bases.
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s,
+                                const GemmArgs *o = nullptr);
 // Small batches, Q4_0 at n_embd 384 / head dim 32, every sentence <= 128 tokens:
 // the int8 QKV of one head and its attention in one workgroup per (head,
 // sentence), bitwise the unfused pair (kernels.hip qkv_attention_small_kernel).

@@ -305,6 +305,15 @@ struct bert_ctx {
     // of f32 rows: MiniLM Q4_0's table 47 -> 6.6 MB, embed_ln 96-98 -> 90-92 us
     // on the headline batch (round 6, profiles/r06_embraw_ab.txt), bitwise equal
     bool emb_raw = true;
+    // the O projection + residual + LayerNorm inside the producer / consumer
+    // kernel after each sentence's attention (kernels.hip qkv_attention_pc_kernel
+    // OT), where that kernel runs and O is on the int8 GEMM: one launch and the
+    // context's HBM round trip fewer per layer, bitwise the separate i8 O + LN
+    // launch (option o_tail).  Default 0: the tail adds 158-160 us to the
+    // fused kernel against 147-151 us for the separate launch (round 6,
+    // profiles/r06_otail_ab.txt): serial after the attention, it has nothing
+    // to overlap with inside the one workgroup per CU
+    bool o_tail = false;
     uint64_t opt_gen = 0;  // bumped by every option change (captured graphs are dropped)
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
@@ -616,7 +625,9 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
     w.tok = w.off = w.rowpos = w.tiles = w.perm = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const int at = ctx->wtype;
-    if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
+    // X too carries GEMM_BM spare rows: the O tail stages 64-row residual halves
+    // from each sentence's first token (rows past the sentence are never stored)
+    if (!dmalloc(w.allocs, &w.X, (size_t)(rows + GEMM_BM) * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
         !dmalloc(w.allocs, &w.qk_lo, (size_t)rows * 2 * E * 2) || !dmalloc(w.allocs, &w.vt_hi, (size_t)rows * E * 2) ||
         !dmalloc(w.allocs, &w.vt_lo, (size_t)rows * E * 2) ||
         !alloc_act(w.allocs, w.Xa, ctx->wtype, rows, E, st) || !alloc_act(w.allocs, w.Ca, at, rows, E, st) ||
@@ -626,7 +637,7 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
         !dmalloc(w.allocs, &w.perm, (size_t)seqs * 4))
         return false;
     // padding rows must hold finite values: zero everything once
-    HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, st));
+    HIP_OK(hipMemsetAsync(w.X, 0, (size_t)(rows + GEMM_BM) * E * 4, st));
     HIP_OK(hipMemsetAsync(w.qk_hi, 0, (size_t)rows * 2 * E * 2, st));
     HIP_OK(hipMemsetAsync(w.qk_lo, 0, (size_t)rows * 2 * E * 2, st));
     HIP_OK(hipMemsetAsync(w.vt_hi, 0, (size_t)rows * E * 2, st));
@@ -706,14 +717,17 @@ bool ws_release(Lane &ln, hipStream_t st) {
 // 1 B/weight, exact isum per block on the int8 MFMA, d_w * d_a applied in
 // the kernel like ggml's vec_dot).  Default: FFN-up (faster than the
 // split-fp16 GEMM) and FFN-down (as fast on full batches, faster on ragged
-// ones) where its LayerNorm is fused (n_embd 384); the O projection stays on
-// the split-fp16 GEMM.  `v` (load option "i8", env
+// ones) where its LayerNorm is fused (n_embd 384); the O projection too for
+// Q4_0 at n_embd 384 (its small-batch tiles beat the split-fp16 ones, and the
+// producer / consumer kernel runs it as its O tail: round 6), elsewhere it
+// stays on the split-fp16 GEMM.  `v` (load option "i8", env
 // BERT_AMD_I8): "0" none, "1" / "all" all three, or a list of up, o, down
 // separated by '+' or ','; empty: the default.
 void i8_select(bert_ctx *ctx, const std::string &spec) {
     // (the down GEMM only where its LayerNorm is fused, E = 384: wider rows use
     // the int8 residual kernel + launch_ln, 8 % slower than split-fp16 on C5)
-    std::string v = spec.empty() ? (ctx->hp.n_embd == 384 ? "up,down" : "up") : spec;
+    std::string v = spec.empty() ? (ctx->hp.n_embd == 384 ? (ctx->wtype == W_Q4_0 ? "up,down,o" : "up,down") : "up")
+                                 : spec;
     std::replace(v.begin(), v.end(), '+', ',');
     const int E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const bool q4 = ctx->wtype == W_Q4_0 || ctx->wtype == W_Q4_1;
@@ -798,12 +812,31 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         aa.scale = 1.0f / sqrtf((float)D);
         aa.expt = half_table(R.exp_tab, R.exp_compact, tables().exp_c);
         aa.ctx = w.Ca;
+        GemmArgs o;
+        o.A = Ca;
+        o.K = E;
+        o.W = L.o;
+        o.N = E;
+        o.bias = L.b_o;
+        o.X = X;
+        o.out_act = Xa;
+        o.ln_w = L.ln1_w;
+        o.ln_b = L.ln1_b;
+        o.eps = hp.eps;
+        if (ctx->i8_o) o.Wi = L.o8;
+        // the O tail (ctx->o_tail): the fused kernel addresses rows absolutely, so
+        // its O arguments get the workspace bases
+        const bool o_tail = fused_qkv_attn && ctx->o_tail && ctx->i8_o && ctx->qkva_ntw == 0 && wt == W_Q4_0 && E == 384;
+        GemmArgs ot = o;
+        ot.A = w.Ca;
+        ot.X = w.X;
+        ot.out_act = w.Xa;
         if (fused_qkv_attn) {
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
             qf.Wi = L.qkv8;  // (qkva_ntw 0)
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st, o_tail ? &ot : nullptr));
         } else if (ctx->i8_qkv && ctx->small_qkva && !ctx->unfused && small && wt == W_Q4_0 && E == 384 && D == 32 &&
                    max_len <= QKVA_SMALL_MAX_LEN && rows <= QKVA_SMALL_ROWS) {
             // one sentence (the server's path): the head's QKV and attention in one kernel
@@ -817,18 +850,9 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
         }
-        GemmArgs o;
-        o.A = Ca;
-        o.K = E;
-        o.W = L.o;
-        o.N = E;
-        o.bias = L.b_o;
-        o.X = X;
-        o.out_act = Xa;
-        o.ln_w = L.ln1_w;
-        o.ln_b = L.ln1_b;
-        o.eps = hp.eps;
-        if (ctx->i8_o) {
+        if (o_tail) {
+            // O + LN ran inside the fused kernel (its O tail)
+        } else if (ctx->i8_o) {
             o.Wi = L.o8;
             if (E == 384) {
                 LAUNCH_OK("gemm_o_ln", gemm_i8(EPI_LN, o));
@@ -1303,6 +1327,8 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         ctx->unfused = value != 0;
     } else if (k == "small_qkva") {
         ctx->small_qkva = value != 0;
+    } else if (k == "o_tail") {
+        ctx->o_tail = value != 0;
     } else if (k == "small_rows" || k == "graph_seqs") {
         if (need(value >= 0, "must be >= 0")) return -2;
         (k == "small_rows" ? ctx->small_rows : ctx->graph_seqs) = value;
@@ -1325,7 +1351,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
     static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows", "graph_seqs",
-                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows", "emb_raw"};
+                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows", "emb_raw", "o_tail"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
         std::string env = "BERT_AMD_" + std::string(k);
@@ -2362,7 +2388,10 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
-        {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw},
+        {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw}, {"o_tail", ctx->o_tail},
+        // resolved: O + LN inside the producer / consumer kernel (run_layer's o_tail,
+        // for the batches that take that kernel)
+        {"o_tail_active", ctx->o_tail && ctx->i8_o && ctx->qkva_ntw == 0 && ctx->wtype == W_Q4_0 && ctx->hp.n_embd == 384},
         // resolved: FFN-up / FFN-down on the bf16 scale products (Q4_1 on the int8 GEMMs)
         {"q41bf_qkv", ctx->wtype == W_Q4_1 && ctx->i8_qkv && q41bf_for(ctx->q41bf, EPI_QKV)},
         {"q41bf_o", ctx->wtype == W_Q4_1 && ctx->i8_o && q41bf_for(ctx->q41bf, ctx->hp.n_embd == 384 ? EPI_LN : EPI_RESID)},

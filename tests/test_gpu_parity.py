@@ -215,7 +215,8 @@ def test_int8_gemm_path_golden(case, mode, model_dir):
     gemm_i8.hip, scales applied in-kernel per block like
     ggml_vec_dot_q4_x_q8_x), and every one on the split-fp16 GEMMs (i8=0),
     against the same golden fixtures, bitwise deterministic (the default
-    mixes the two: up and down int8, o split-fp16)."""
+    mixes the two: Q4_0 MiniLM runs QKV / O / up / down on int8, Q4_1 MiniLM
+    up / down, with QKV and O split-fp16)."""
     meta, toks, want = load_case(case)
     p = ensure_model(model_dir, meta["shape"], meta["ftype"], meta["w_std"], meta.get("n_layer"))
     m = bertlib.BertModel(p, options={"i8": mode})
@@ -1049,6 +1050,49 @@ def test_producer_consumer_kernel(model_dir):
         m0.close()
         m2.close()
 
+
+
+def test_o_tail_bitwise_separate_o_launch(model_dir):
+    """The O tail (option o_tail; default 0, measured slower): where the producer / consumer
+    kernel runs, its 12 waves finish each sentence with the O projection +
+    residual + LayerNorm (int8 O, i8_ln384_kernel's main loop and LayerNorm)
+    instead of a separate gemm_o_ln launch.  The residual stream X and its Q8
+    form after every layer, and the embeddings, are bitwise those of the
+    separate launch: sentences of 2..128 tokens (one or two 64-row halves),
+    packed tiles of short sentences, full 128-token sentences, and a batch whose
+    last sentence ends off the 128-row padding (the tail's halves read rows past
+    it, never store them).  Reference: bert.cpp:944-962."""
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    m = bertlib.BertModel(p)
+    try:
+        assert m.get_option("i8_o") == 1 and m.get_option("qkva_ntw") == 0
+        assert m.get_option("o_tail") == 0 and m.get_option("o_tail_active") == 0
+        m.set_option("o_tail", 1)
+        assert m.get_option("o_tail_active") == 1
+        rng = np.random.default_rng(77)
+        batches = [[[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in rng.integers(2, 129, 300)],
+                   [[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in rng.integers(2, 41, 500)],
+                   [sentence(900 + i, 128, 30522) for i in range(64)],
+                   [sentence(1000 + i, 65 + i, 30522) for i in range(50)] + [sentence(7, 3, 30522)]]
+        for bi, toks in enumerate(batches):
+            got = {}
+            for ot in (1, 0):
+                m.set_option("o_tail", ot)
+                got[ot] = m.eval_batch(toks)
+            m.set_option("o_tail", 1)
+            bad = [i for i in range(len(toks)) if not np.array_equal(got[1][i], got[0][i])]
+            assert not bad, (bi, bad[:10], [len(toks[i]) for i in bad[:10]])
+            assert np.all(np.isfinite(got[1]))
+        toks = batches[0][:60]
+        layers = {}
+        for ot in (1, 0):
+            m.set_option("o_tail", ot)
+            layers[ot] = m.debug_layers(toks)
+        m.set_option("o_tail", 1)
+        for a, b, name in zip(layers[1], layers[0], ("X", "q", "d")):
+            assert np.array_equal(a, b), name
+    finally:
+        m.close()
 
 
 @pytest.mark.parametrize("shape,ftype,n_layer,vocab", [("e5-base", "f16", 1, 250002), ("bge-large", "q4_1", 2, 30522)])
