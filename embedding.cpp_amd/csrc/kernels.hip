@@ -1297,11 +1297,18 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 #define QKVA_SMALL 1
 #endif
 
+// LNP (LayerNorm on read, GemmArgs ln_in): the sentence's A rows are Q8(LN(g.X))
+// made here (ln384_rows_to_lds, bitwise the LayerNorm pass + Q8 store), the
+// head-0 workgroup writing the f32 LN output to g.Xln.
+template <bool LNP>
 __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, AttnArgs a) {
     constexpr int D = 32, E = 384, NKB = E / 32, NK = 128, KST = D + 8, VST = NK + 4;
     __shared__ __attribute__((aligned(16))) _Float16 Qh[NK * KST], Ql[NK * KST], Kh[NK * KST], Kl[NK * KST];
     __shared__ __attribute__((aligned(16))) _Float16 Vh[D * VST], Vl[D * VST];
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
+    __shared__ __attribute__((aligned(16))) int8_t aq[LNP ? NK * E : 16];
+    __shared__ uint16_t ad[LNP ? NK * NKB : 8];
+    __shared__ double lpart[LNP ? 48 * 2 * 12 : 1];
     const int h = blockIdx.x, s = blockIdx.y;
     const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
     if (n > NK || n <= 0 || g.K != E || a.E != E) return;
@@ -1309,6 +1316,10 @@ __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, At
     const int nt = (n + 31) >> 5;
     const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
     for (int i = tid; i < a.expt.n_pad / 8; i += 768) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
+    if constexpr (LNP) {  // rows beg .. beg + 32 nt - 1 (past the sentence: masked keys, never stored)
+        ln384_rows_to_lds<2>(g.X, beg, 32 * nt, n, g.ln_w, g.ln_b, g.eps, aq, ad, h == 0 ? g.Xln : nullptr, lpart);
+        __syncthreads();
+    }
 
     if (wv < 3 * nt) {
         const int rt = wv / 3, part = wv - 3 * rt, ft0 = 3 * h + part;  // head-major f-tile of Q | K | V
@@ -1320,9 +1331,15 @@ __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, At
         auto load = [&](int b) {
             const int sl = b % RING;
             wq[sl] = i8_wq(g.Wi, NKB, ft0, b);
-            xa[sl] = *(const int4v *)((const int8_t *)g.A.q + row * E + 32 * b + 16 * hh);
             dw[sl] = ((const uint16_t *)g.Wi.dh)[(((int64_t)ft0 * (NKB >> 2) + (b >> 2)) * 32 + r) * 4 + (b & 3)];
-            da[sl] = ((const uint16_t *)g.A.d)[row * NKB + b];
+            if constexpr (LNP) {
+                const int lr = 32 * rt + r;
+                xa[sl] = *(const int4v *)(aq + lr * E + 32 * b + 16 * hh);
+                da[sl] = ad[lr * NKB + b];
+            } else {
+                xa[sl] = *(const int4v *)((const int8_t *)g.A.q + row * E + 32 * b + 16 * hh);
+                da[sl] = ((const uint16_t *)g.A.d)[row * NKB + b];
+            }
         };
 #pragma unroll
         for (int b = 0; b < RING; b++) load(b);
@@ -1429,7 +1446,12 @@ __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, At
 
 hipError_t launch_qkv_attention_small(const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
     if (!QKVA_SMALL || g.K != 384 || a.E != 384 || a.H * 32 != a.E || n_seqs <= 0) return hipErrorNotSupported;
-    hipLaunchKernelGGL(qkv_attention_small_kernel, dim3(a.H, n_seqs), dim3(768), 0, s, g, a);
+    if (g.ln_in) {
+        if (!g.Xln) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(qkv_attention_small_kernel<true>, dim3(a.H, n_seqs), dim3(768), 0, s, g, a);
+    } else {
+        hipLaunchKernelGGL(qkv_attention_small_kernel<false>, dim3(a.H, n_seqs), dim3(768), 0, s, g, a);
+    }
     return hipGetLastError();
 }
 
@@ -2605,6 +2627,58 @@ hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E
                        const int32_t *out_row) {
     if (E > 1024) return hipErrorInvalidValue;
     hipLaunchKernelGGL(pool_l2_kernel, dim3(n_seqs), dim3(256), 0, s, X, offsets, E, out, out_row);
+    return hipGetLastError();
+}
+
+// pool_l2_kernel over LN(X) (LayerNorm on read of the last layer's residual
+// sums, E = 384): the sentence's rows in chunks of 32, each normalised by one
+// wave into LDS (ln384_row_wave: bitwise the LayerNorm pass), then pooled in
+// row order exactly as pool_l2_kernel.
+__global__ __launch_bounds__(1024) void pool_l2_ln_kernel(const float *X, const int32_t *offsets, const float *ln_w,
+                                                          const float *ln_b, float eps, float *out,
+                                                          const int32_t *out_row) {
+    constexpr int E = 384, CH = 32;  // 16 waves: one 32-row chunk per pass (two rows a wave)
+    __shared__ __attribute__((aligned(16))) float ys[CH * E];
+    __shared__ __attribute__((aligned(16))) int8_t aq[CH * E];  // (the Q8 form: unused here)
+    __shared__ uint16_t ad[CH * 12];
+    __shared__ double lpart[48 * 16];
+    __shared__ double red[16];
+    const int s = blockIdx.x, tid = threadIdx.x, c = 4 * tid;
+    const int beg = offsets[s], n = offsets[s + 1] - beg;
+    const float invN = 1.0f / n;
+    float4v acc = {0.f, 0.f, 0.f, 0.f};
+    for (int t0 = 0; t0 < n; t0 += CH) {
+        const int nc = min(CH, n - t0);
+        ln384_rows_to_lds<1>(X, (int64_t)beg + t0, nc, 0, ln_w, ln_b, eps, aq, ad, nullptr, lpart, ys);
+        __syncthreads();
+        if (c < E) {
+            for (int t = 0; t < nc; t++) {
+                const float4v x = *(const float4v *)(ys + t * E + c);
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[j] = fmaf(x[j], invN, acc[j]);
+            }
+        }
+        __syncthreads();
+    }
+    // pool_l2_kernel's norm: its 96 active threads sit in its first two waves
+    // (lanes 0-63, 64-95); the others add zeros, so red[0] + red[1] (+ 0 + 0) is its sum
+    double ss = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) ss += (double)(acc[j] * acc[j]);
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    const double tot = red[0] + red[1] + red[2] + red[3];
+    const float len = sqrtf((float)tot);
+    const float r = 1.0f / len;
+    const int64_t orow = out_row ? out_row[s] : s;
+    if (c < E) *(float4v *)(out + orow * E + c) = float4v{acc[0] * r, acc[1] * r, acc[2] * r, acc[3] * r};
+}
+
+hipError_t launch_pool_ln(const float *X, const int32_t *offsets, int n_seqs, int E, const float *ln_w,
+                          const float *ln_b, float eps, float *out, hipStream_t s, const int32_t *out_row) {
+    if (E != 384) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pool_l2_ln_kernel, dim3(n_seqs), dim3(1024), 0, s, X, offsets, ln_w, ln_b, eps, out, out_row);
     return hipGetLastError();
 }
 

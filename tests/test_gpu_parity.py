@@ -1095,6 +1095,45 @@ def test_o_tail_bitwise_separate_o_launch(model_dir):
         m.close()
 
 
+def test_ln_on_read_bitwise(model_dir):
+    """LayerNorm on read (option ln_read; default 0, measured slower): small Q4_0 batches (<= 512
+    padded rows) run the O and FFN-down LayerNorms inside the kernel that reads
+    their output (FFN-up's A rows, the next layer's QKV A rows, the pooling)
+    instead of as passes of their own: the embeddings are bitwise those of the
+    LayerNorm passes, through the fused small QKV + attention kernel (<= 64
+    tokens) and the K-split QKV GEMM (65..128), alone and in small batches,
+    with 2 x n_layer launches fewer per call.  Reference: bert.cpp:944-962,
+    :973-992 (ggml_norm after the residual adds)."""
+    p, _ = get_model(model_dir, "minilm", "q4_0")
+    m = bertlib.BertModel(p)
+    try:
+        assert m.get_option("ln_read") == 0
+        n_layer = m.hparams[5]
+        rng = np.random.default_rng(5)
+        batches = [[sentence(300 + n, n, 30522)] for n in (2, 16, 33, 64, 65, 100, 128)]
+        batches += [[sentence(400 + i, int(n), 30522) for i, n in enumerate(rng.integers(2, 65, 7))],
+                    [sentence(500 + i, int(n), 30522) for i, n in enumerate(rng.integers(2, 129, 4))]]
+        for toks in batches:
+            got, launches = {}, {}
+            for lr in (1, 0):
+                m.set_option("ln_read", lr)
+                got[lr] = m.eval_batch(toks)
+                m.profile(True)
+                m.eval_batch(toks)
+                launches[lr] = sum(c for _, c in m.profile_read().values())
+                m.profile(False)
+            m.set_option("ln_read", 0)
+            lens = [len(t) for t in toks]
+            assert np.array_equal(got[1], got[0]), lens
+            assert np.all(np.isfinite(got[1])), lens
+            assert launches[0] - launches[1] == 2 * n_layer, (lens, launches)
+            m.set_option("ln_read", 1)
+            assert np.array_equal(m.eval(toks[0]), got[1][0]), lens  # bert_eval: the same small path
+            m.set_option("ln_read", 0)
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("shape,ftype,n_layer,vocab", [("e5-base", "f16", 1, 250002), ("bge-large", "q4_1", 2, 30522)])
 def test_long_attention_head_dim_64_mixed_lengths(shape, ftype, n_layer, vocab, model_dir):
     """Head dim 64 on the unfused pair (option unfused) with sentences of
