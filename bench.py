@@ -177,15 +177,13 @@ def kernel_parts(name: str, B: int, N: int, hp: dict, arith: dict, ftype: str) -
     qkv_int8 = q4 and bool(arith["i8_qkv"] if "i8_qkv" in arith else arith.get("qkva_ntw") == 0)
     qkv = (2.0 * M * E * 3 * E, PEAK_INT8_TOPS if qkv_int8 else gemm_peak)
     att = (4.0 * B * N * N * E, PEAK_FP16_TFLOPS)
-    # o_tail_active: the producer / consumer kernel also runs O + LN (int8 O)
-    o_tail = [(2.0 * M * E * E, PEAK_INT8_TOPS)] if arith.get("o_tail_active") else []
     return {
         "gemm_qkv": [qkv],
         "gemm_o_ln": [(2.0 * M * E * E, proj("i8_o"))],
         "gemm_up_gelu": [(2.0 * M * E * I, proj("i8_up"))],
         "gemm_down_ln": [(2.0 * M * I * E, proj("i8_down"))],
         "attention": [att],
-        "qkv_attention": [qkv, att] + o_tail,
+        "qkv_attention": [qkv, att],
     }.get(name, [])
 
 
@@ -218,8 +216,6 @@ def dtype_note(ftype: str, arith: dict) -> str:
                                          "on fp16 MFMA (per-block d_a fold)")
     else:
         s = f"{ftype} GEMM on {'fp16' if ftype == 'f16' else 'f32'} MFMA, f32 accumulate"
-    if arith.get("o_tail_active"):
-        s += "; O + LN inside the fused QKV + attention kernel (its O tail)"
     return s + "; attention split-fp16 MFMA (f32-level); LN/softmax sums f64"
 
 
@@ -236,12 +232,8 @@ def mixed_roofline(parts: list, avg_s: float) -> dict:
                 parts=[dict(flops=f, peak=p) for f, p in parts])
 
 
-def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str, arith: dict | None = None) -> float:
-    """Algorithmic HBM bytes per launch (each operand read once, each output
-    written once).  With the O tail (arith["o_tail_active"]) the fused kernel
-    reads Xa and the residual X and writes X and Xa; its context stays inside
-    the kernel (stored and read back by the same workgroup)."""
-    o_tail = bool(arith and arith.get("o_tail_active"))
+def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str) -> float:
+    """Algorithmic HBM bytes per launch (each operand read once, each output written once)."""
     E, I, L = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
     M = B * N
     act = {"q4_0": 1 + 2 / 32, "q4_1": 1 + 4 / 32, "f16": 2, "f32": 4}[ftype]  # bytes/elem of GEMM inputs
@@ -252,8 +244,7 @@ def kernel_bytes(name: str, B: int, N: int, hp: dict, ftype: str, arith: dict | 
         "gemm_up_gelu": M * E * act + E * I * wb + M * I * act,
         "gemm_down_ln": M * I * act + E * I * wb + 2 * M * E * 4 + M * E * act,
         "attention": M * 3 * E * 4 + M * E * act,
-        "qkv_attention": (M * E * act + 4 * E * E * wb + 2 * M * E * 4 + M * E * act) if o_tail
-        else M * E * act + 3 * E * E * wb + M * E * act,
+        "qkv_attention": M * E * act + 3 * E * E * wb + M * E * act,
         "embed_ln": M * 4 + M * E * (4 + act) + M * E * 4,  # f32 word rows (pos/type tables stay cached)
         "pool_l2": M * E * 4 + B * E * 4,
     }.get(name, 0.0) if L else 0.0
@@ -479,11 +470,11 @@ def main():
     model.profile(False)
     model.set_option("split", int(os.environ.get("BERT_AMD_SPLIT", "1")[:1] != "0"))
     arith = {k: model.get_option(k) for k in ("qkva_ntw", "i8_qkv", "i8_up", "i8_o", "i8_down", "q41bf_qkv",
-                                              "q41bf_o", "q41bf_up", "q41bf_down", "o_tail_active")}
+                                              "q41bf_o", "q41bf_up", "q41bf_down")}
     kern = {}
     for name, (ms, cnt) in prof.items():
         parts = kernel_parts(name, B, N, hp, arith, args.ftype)
-        by = kernel_bytes(name, B, N, hp, args.ftype, arith)
+        by = kernel_bytes(name, B, N, hp, args.ftype)
         avg_s = ms / max(cnt, 1) / 1e3
         kern[name] = dict(avg_us=round(avg_s * 1e6, 2), launches_per_step=cnt // max(args.profile_steps, 1),
                           share=round(ms / max(sum(v[0] for v in prof.values()), 1e-9), 4),
@@ -504,7 +495,7 @@ def main():
             roofline = dict(kernel=dominant, bound="mfma", unit="TFLOP/s", **mixed_roofline(parts, avg_s),
                             formula="frac = sum(F_i / peak_i) / t_launch; peak = F / sum(F_i / peak_i)")
         else:
-            by = kernel_bytes(dominant, B, N, hp, args.ftype, arith)
+            by = kernel_bytes(dominant, B, N, hp, args.ftype)
             ach = by / avg_s / 1e9
             roofline = dict(kernel=dominant, bound="hbm", achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                             frac=round(ach / PEAK_HBM_GBS, 4), bytes_per_launch=by)
@@ -541,7 +532,7 @@ def main():
                             frac=round(gbs / PEAK_HBM_GBS, 4), stale=bool(stale),
                             source=f"profiles/pmc_traffic.json ({pt.get('source', '')}; git {pt.get('git_head', '?')}) "
                                    f"over this run's ms_per_step")
-        roofline["algorithmic_bytes_per_launch"] = kernel_bytes(dominant, B, N, hp, args.ftype, arith)
+        roofline["algorithmic_bytes_per_launch"] = kernel_bytes(dominant, B, N, hp, args.ftype)
 
     # whole-path MFMA fraction: F(N) = L(8NE^2 + 4NEI + 4N^2E) per sentence
     E, I, L = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]

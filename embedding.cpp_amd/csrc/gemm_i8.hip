@@ -129,9 +129,7 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
 // the chunk starts), and the previous tile's LN output leaves xs during the same
 // chunks, each wave draining one 1 KiB piece of xs to X just before refilling
 // that piece with the new residual; the last tile's output leaves after the loop.
-// (i8_xs_chunk: i8_core.h.  The LN epilogue below is i8_ln384_epilogue of i8_core.h
-// written out, the same arithmetic in the same order: qkv_attention_pc_kernel's O tail
-// runs that helper and tests/test_gpu_parity.py checks the two bitwise.)
+__device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ (r & 15)); }
 
 #ifndef I8_LN_OV
 #define I8_LN_OV 1
@@ -643,17 +641,10 @@ __global__ __launch_bounds__(NW * 64) void i8_small_kernel(GemmArgs g, int n_mti
 #define I8_KS_NW48 16
 #endif
 
-// LNP (LayerNorm on read, GemmArgs ln_in; K = 384): the tile's 32 A rows are
-// Q8(LN(g.X)) made in the kernel (ln384_rows_to_lds: i8_ln384_rows_kernel's
-// arithmetic, bitwise), the workgroups of f-tile 0 writing the f32 LN output to
-// g.Xln; the weight operands are in flight meanwhile.
-template <int EPI, int NW, int R, bool LNP = false>
+template <int EPI, int NW, int R>
 __global__ __launch_bounds__(NW * 64) void i8_small_ks_kernel(GemmArgs g, int n_mtiles, int n_ntiles) {
     constexpr int NT = NW * 64, PER = (1024 + NT - 1) / NT;
     __shared__ float fis[NW][1024], fdd[NW][1024];  // [wave][i 64 + lane]
-    __shared__ __attribute__((aligned(16))) int8_t aq[LNP ? 32 * 384 : 16];
-    __shared__ uint16_t ad[LNP ? 32 * 12 : 8];
-    __shared__ double lpart[LNP ? 48 * 2 * NW : 1];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int nwg = n_mtiles * n_ntiles;
     if ((int)blockIdx.x >= nwg) return;
@@ -668,21 +659,9 @@ __global__ __launch_bounds__(NW * 64) void i8_small_ks_kernel(GemmArgs g, int n_
     for (int r = 0; r < R; r++) {
         const int b = min(NW * r + wv, nkb - 1);  // clamped: a wave past the last block loads and drops it
         wq[r] = i8_wq(g.Wi, nkb, ft0, b);
-        if constexpr (!LNP) xa[r] = *(const int4v *)((const int8_t *)g.A.q + row * K + 32 * b + 16 * hh);
+        xa[r] = *(const int4v *)((const int8_t *)g.A.q + row * K + 32 * b + 16 * hh);
         dw[r] = ((const uint16_t *)g.Wi.dh)[(((int64_t)ft0 * (nkb >> 2) + (b >> 2)) * 32 + l32) * 4 + (b & 3)];
-        if constexpr (!LNP) da[r] = ((const uint16_t *)g.A.d)[row * nkb + b];
-    }
-    if constexpr (LNP) {
-        static_assert(R == 1, "LayerNorm on read: K = 384 over 12 waves");
-        ln384_rows_to_lds<2>(g.X, (int64_t)mt * 32, 32, 32, g.ln_w, g.ln_b, g.eps, aq, ad, ft0 == 0 ? g.Xln : nullptr,
-                             lpart);
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int b = min(NW * r + wv, nkb - 1);
-            xa[r] = *(const int4v *)(aq + l32 * 384 + 32 * b + 16 * hh);
-            da[r] = ad[l32 * 12 + b];
-        }
+        da[r] = ((const uint16_t *)g.A.d)[row * nkb + b];
     }
     I8EpiPre pre;  // the epilogue's global operands, issued with the block operands (wave 0's)
     if (wv == 0) i8_small_epi_pre<EPI>(g, row, ft0, hh, pre);
@@ -877,12 +856,6 @@ static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s
             const int ntk = a.N / 32;
             auto go = [&](auto kern, int nw) { hipLaunchKernelGGL(kern, gk, dim3(nw * 64), 0, s, a, mt, ntk); };
             const int e2 = epi == EPI_LN ? EPI_RESID : epi;
-            if (a.ln_in) {  // LayerNorm on read: the 384-wide A rows of FFN-up / QKV
-                if (nkb != 12 || (e2 != EPI_GELU_ACT && e2 != EPI_QKV) || !a.Xln) return hipErrorInvalidValue;
-                if (e2 == EPI_GELU_ACT) go(i8_small_ks_kernel<EPI_GELU_ACT, 12, 1, true>, 12);
-                else go(i8_small_ks_kernel<EPI_QKV, 12, 1, true>, 12);
-                return hipGetLastError();
-            }
 #define I8_KS_GO(E)                                                                       \
     (nkb <= 12 ? go(i8_small_ks_kernel<E, 12, 1>, 12)                                  \
                : nkb <= 48 ? go(i8_small_ks_kernel<E, I8_KS_NW48, 48 / I8_KS_NW48>, I8_KS_NW48)             \
@@ -894,7 +867,7 @@ static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s
                 default: return hipErrorInvalidValue;
             }
 #undef I8_KS_GO
-            if (epi == EPI_LN && !a.defer_ln) {  // (defer_ln: the next kernel normalises on read)
+            if (epi == EPI_LN && !a.defer_ln) {  // (defer_ln: the caller launches the LayerNorm pass)
                 const hipError_t e = hipGetLastError();
                 if (e != hipSuccess) return e;
                 hipLaunchKernelGGL((i8_ln384_rows_kernel<WT>), dim3(Mpad / 4), dim3(256), 0, s, a, Mpad);
@@ -902,7 +875,6 @@ static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s
             return hipGetLastError();
         }
     }
-    if (a.ln_in) return hipErrorInvalidValue;  // LayerNorm on read: the K-split kernels only
     switch (epi) {
         case EPI_QKV:
             if (a.head_dim <= 0 || a.head_dim % 16 || (a.N / 3) % a.head_dim) return hipErrorInvalidValue;
@@ -912,7 +884,7 @@ static hipError_t i8_small_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s
         case EPI_RESID: hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW, SEG>), grid, block, 0, s, a, mt, nt); break;
         case EPI_LN: {
             hipLaunchKernelGGL((i8_small_kernel<WT, EPI_RESID, NW, SEG>), grid, block, 0, s, a, mt, nt);
-            if (a.defer_ln) break;  // the caller runs the LayerNorm (launch_ln384_rows_i8) or normalises on read
+            if (a.defer_ln) break;  // the caller launches the LayerNorm pass (launch_ln384_rows_i8)
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL((i8_ln384_rows_kernel<WT>), dim3(Mpad / 4), dim3(256), 0, s, a, Mpad);
@@ -933,8 +905,6 @@ hipError_t launch_ln384_rows_i8(int wtype, const GemmArgs &a, int Mpad, hipStrea
     }
     return hipGetLastError();
 }
-
-bool i8_small_ln_on_read(int wtype, int Mpad) { return I8_KS && wtype == W_Q4_0 && Mpad % 32 == 0 && Mpad <= I8_KS_ROWS; }
 
 hipError_t launch_gemm_i8_small(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
     if (!i8_gemm_supported(epi, a.N, a.K) || Mpad % 128) return hipErrorInvalidValue;

@@ -448,231 +448,6 @@ __device__ __forceinline__ void i8_store_q8_half(const ActPtr &out, int64_t ld, 
     }
 }
 
-// ggml quantize_row_q8_0 of the 32-value block held as 16 values by lanes l and
-// l ^ 32 (i8_store_q8_half's arithmetic, into storage of the caller's choice):
-// lane half hh's 16 bytes and the block's scale d.
-__device__ __forceinline__ void q8_half_pack(const float (&y)[16], uint4 &pk, float &d) {
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; i++) amax = fmaxf(amax, fabsf(y[i]));
-    {
-        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
-        amax = fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
-    }
-    float id;
-    q8_scales(amax, d, id);
-    pk.x = q8_pack4(y[0], y[1], y[2], y[3], id);
-    pk.y = q8_pack4(y[4], y[5], y[6], y[7], id);
-    pk.z = q8_pack4(y[8], y[9], y[10], y[11], id);
-    pk.w = q8_pack4(y[12], y[13], y[14], y[15], id);
-}
-
-// LayerNorm on read (small batches, Q4_0 at n_embd 384): ggml_norm + the affine
-// of 384-wide f32 rows with i8_ln384_rows_kernel's arithmetic and reduction
-// order.  A wave handles two rows per pass: lanes (w = lane & 31, hh = lane >> 5)
-// with w < 12 hold row A's columns 32 w + 16 hh .. + 15, lanes with 12 <= w < 24
-// row B's columns 32 (w - 12) + 16 hh ..; double sums over the lane's 16 in
-// order, the lane-half pair, then the row's twelve pair sums in order through
-// `part` (LDS owned by the wave; its own accesses run in order, no workgroup
-// barrier).  RB passes share one batch of loads (their latencies overlap).
-// Rows row0 + rr, rr = 2 wave + sub + 2 nw k (< nrows): the LN output quantised
-// to Q8_0 into an LDS A tile (aq [nrows][384] bytes, ad [nrows][12] fp16: the
-// activation rows' global layout) and, when xln is non-null, the f32 LN output
-// to xln (rows < nstore).  part_all: 48 RB doubles per wave.  The caller's
-// barrier publishes the tile.  ys (optional): the f32 LN output into LDS rows
-// [rr][384] as well.
-template <int RB>
-__device__ __forceinline__ void ln384_rows_to_lds(const float *X, int64_t row0, int nrows, int nstore,
-                                                  const float *ln_w, const float *ln_b, float eps, int8_t *aq,
-                                                  uint16_t *ad, float *xln, double *part_all, float *ys = nullptr) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6, w = lane & 31, hh = lane >> 5;
-    const int sub = w >= 12, blk = w < 12 ? w : w < 24 ? w - 12 : 0;  // (lanes 24..31: a copy of row B's block 0)
-    const bool own = w < 24;
-    const int col = 32 * blk + 16 * hh;
-    float4v lw[4], lb[4];
-#pragma unroll
-    for (int qq = 0; qq < 4; qq++) {
-        lw[qq] = *(const float4v *)(ln_w + col + 4 * qq);
-        lb[qq] = *(const float4v *)(ln_b + col + 4 * qq);
-    }
-    double *part = part_all + 48 * RB * wv;
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    for (int base = 2 * wv; base < nrows; base += 2 * nw * RB) {
-        float v[RB][16];
-        int rr[RB];
-#pragma unroll
-        for (int k = 0; k < RB; k++) {
-            rr[k] = base + 2 * nw * k + sub;
-            const int rl = rr[k] < nrows ? rr[k] : base;  // (a row past the tile: reload row `base`, unused)
-            const float *xr = X + (row0 + rl) * 384 + col;
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                const float4v x4 = *(const float4v *)(xr + 4 * qq);
-#pragma unroll
-                for (int j = 0; j < 4; j++) v[k][4 * qq + j] = x4[j];
-            }
-        }
-        // slot of (pass k, row of this lane, statistic j) in part: 12 doubles
-        auto slot = [&](int k, int j) { return part + ((2 * k + sub) * 2 + j) * 12; };
-        float mean[RB], scale[RB];
-#pragma unroll
-        for (int k = 0; k < RB; k++) {
-            double s = 0.0;
-#pragma unroll
-            for (int i = 0; i < 16; i++) s += (double)v[k][i];
-            s += __shfl_xor(s, 32);
-            if (own && hh == 0) slot(k, 0)[blk] = s;
-        }
-        wave_sync();
-#pragma unroll
-        for (int k = 0; k < RB; k++) {
-            double tot = 0.0;
-#pragma unroll
-            for (int q = 0; q < 12; q++) tot += slot(k, 0)[q];
-            mean[k] = (float)(tot / 384);
-            double s2 = 0.0;
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                v[k][i] = v[k][i] - mean[k];
-                s2 += (double)(v[k][i] * v[k][i]);
-            }
-            s2 += __shfl_xor(s2, 32);
-            if (own && hh == 0) slot(k, 1)[blk] = s2;
-        }
-        wave_sync();
-#pragma unroll
-        for (int k = 0; k < RB; k++) {
-            double tot = 0.0;
-#pragma unroll
-            for (int q = 0; q < 12; q++) tot += slot(k, 1)[q];
-            const float var = (float)(tot / 384);
-            scale[k] = 1.0f / sqrtf(var + eps);
-            float y[16];
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    float z = v[k][4 * qq + j] * scale[k];
-                    z = lw[qq][j] * z;
-                    y[4 * qq + j] = z + lb[qq][j];
-                }
-            uint4 pk;
-            float d;
-            q8_half_pack(y, pk, d);
-            if (own && rr[k] < nrows) {
-                const int r = rr[k];
-                *(uint4 *)(aq + r * 384 + 32 * blk + 16 * hh) = pk;
-                if (hh == 0) ad[r * 12 + blk] = f2h(d);
-                if (ys) {
-#pragma unroll
-                    for (int qq = 0; qq < 4; qq++)
-                        *(float4v *)(ys + r * 384 + col + 4 * qq) = float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
-                }
-                if (xln && r < nstore) {
-                    float *xo = xln + (row0 + r) * 384 + col;
-#pragma unroll
-                    for (int qq = 0; qq < 4; qq++)
-                        *(float4v *)(xo + 4 * qq) = float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
-                }
-            }
-        }
-        wave_sync();  // (the next batch rewrites part)
-    }
-}
-
-// 16-byte chunk c of row r of a 64-row x 384-feature f32 tile in LDS (the LN
-// kernels' residual tile): chunk c ^ (r & 15), so row-per-lane reads are
-// conflict-free.
-__device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ (r & 15)); }
-
-// The LayerNorm epilogue of a 64-row x 384-feature tile (bert.cpp:944-962 and
-// :973-992): X = LN((b + W.x) + X).  12 waves; wave w holds acc[0][t] = features
-// 32 w + 16 hh .. + 15 of token 32 t + (lane & 31); the residual tile is in xs
-// (i8_xs_chunk layout) and the LN output replaces it there; the Q8 form goes to
-// g.out_act (rows m0 ..).  ggml_norm's double sums go lane -> lane pair -> the
-// twelve waves (red: [2][12][64], fixed order).  Shared by i8_ln384_kernel and
-// the O tail of qkv_attention_pc_kernel, so the two are bitwise equal.  MASK:
-// rows >= nvalid are computed but their Q8 form is not stored.  Starts after a
-// barrier that published xs; contains two barriers; ends after its stores.
-template <int WT, bool MASK>
-__device__ __forceinline__ void i8_ln384_epilogue(float16v (&acc)[1][2], float *xs, double (*red)[12][64],
-                                                  const GemmArgs &g, int64_t m0, int nvalid, int it) {
-    constexpr int T = 2, NCOL = 384, NWV = 12;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l32 = lane & 31, hh = lane >> 5;
-    const int ft0 = wv, col = 32 * ft0 + 16 * hh;
-    // v = (b + W.x) + x  (ggml: add(repeat(b), mul_mat) then add(cur, inpL))
-#pragma unroll
-    for (int t = 0; t < T; t++) {
-        const int r = 32 * t + l32;
-        double s = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const float4v x4 = *(const float4v *)(xs + 4 * i8_xs_chunk(r, (col >> 2) + qq));
-            const float4v b4 = *(const float4v *)(g.bias + col + 4 * qq);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float v = (b4[j] + acc[0][t][4 * qq + j]) + x4[j];
-                acc[0][t][4 * qq + j] = v;
-                s += (double)v;
-            }
-        }
-        s += __shfl_xor(s, 32);
-        if (hh == 0) red[0][wv][r] = s;
-    }
-    __syncthreads();
-    STAMP(it, 3, NWV);
-    float mean[T];
-#pragma unroll
-    for (int t = 0; t < T; t++) {
-        const int r = 32 * t + l32;
-        double tot = 0.0;
-#pragma unroll
-        for (int w = 0; w < NWV; w++) tot += red[0][w][r];
-        mean[t] = (float)(tot / NCOL);
-        double s2 = 0.0;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const float v = acc[0][t][i] - mean[t];
-            acc[0][t][i] = v;
-            s2 += (double)(v * v);
-        }
-        s2 += __shfl_xor(s2, 32);
-        if (hh == 0) red[1][wv][r] = s2;
-    }
-    __syncthreads();
-    STAMP(it, 4, NWV);
-#pragma unroll
-    for (int t = 0; t < T; t++) {
-        const int r = 32 * t + l32;
-        const int64_t row = m0 + r;
-        double tot = 0.0;
-#pragma unroll
-        for (int w = 0; w < NWV; w++) tot += red[1][w][r];
-        const float var = (float)(tot / NCOL);
-        const float scale = 1.0f / sqrtf(var + g.eps);
-        float y[16];
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const float4v w4 = *(const float4v *)(g.ln_w + col + 4 * qq);
-            const float4v b4 = *(const float4v *)(g.ln_b + col + 4 * qq);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                float z = acc[0][t][4 * qq + j] * scale;
-                z = w4[j] * z;
-                y[4 * qq + j] = z + b4[j];
-            }
-            // in place: each (row, chunk) is this lane's alone
-            *(float4v *)(xs + 4 * i8_xs_chunk(r, (col >> 2) + qq)) =
-                float4v{y[4 * qq], y[4 * qq + 1], y[4 * qq + 2], y[4 * qq + 3]};
-        }
-        if (!MASK || r < nvalid) i8_store_q8_half<WT>(g.out_act, NCOL, row, ft0, hh, y);
-    }
-}
-
 // XCD-aware tile order (as gemm_kernel): linear ids are dealt round-robin over
 // the 8 XCDs; each XCD walks a contiguous range, n fastest.
 __device__ __forceinline__ int xcd_linear(int orig, int nwg) {
@@ -729,12 +504,9 @@ struct I8ResRing {
     }
 };
 
-// hook(c, nch) runs at the start of every chunk c (the caller's memory traffic
-// interleaved with the main loop, as in i8_mainloop).
-template <int WT, int BM, int F, int T, int AH, typename Hook = I8NoHook>
+template <int WT, int BM, int F, int T, int AH>
 __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const char *apanel, int ft0, int tt0,
-                                                     float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn,
-                                                     const Hook &hook = Hook()) {
+                                                     float16v (&acc)[F][T], I8ResRing<WT, F, AH> &ring, int ftn) {
     constexpr bool Q1 = wt_q41(WT);
     using C = I8Chunk<BM, Q1, WT == W_Q4_1B>;
     const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -762,7 +534,6 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
         const int b0 = 4 * c;
         const bool last = c + 1 == nch;
         const char *buf = apanel + c * C::BYTES;
-        hook(c, nch);
         wscale_use();
         if (!last) ring.sload(g, ft0, c + 1);
         else if (ftn >= 0) ring.sload(g, ftn, 0);

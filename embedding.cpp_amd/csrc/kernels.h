@@ -118,14 +118,9 @@ struct GemmArgs {
     const float *ln_w = nullptr, *ln_b = nullptr;
     float eps = 0.f;
     HalfTable gelu;                      // EPI_GELU_ACT: ggml's fp16 GELU table
-    // LayerNorm on read (small batches, Q4_0 at n_embd 384; launch_gemm_i8_small,
-    // launch_qkv_attention_small): defer_ln (EPI_LN): leave (b + W.x) + X in X,
-    // no LayerNorm pass; ln_in (EPI_GELU_ACT / EPI_QKV, K = 384): the A operand
-    // is Q8(LN(X)) with ln_w / ln_b / eps, computed in the kernel (bitwise the
-    // LayerNorm pass + Q8 store), and the f32 LN output goes to Xln (written by
-    // one workgroup per row)
-    int defer_ln = 0, ln_in = 0;
-    float *Xln = nullptr;
+    // EPI_LN in launch_gemm_i8_small: leave (b + W.x) + X in X; the caller runs
+    // the LayerNorm pass (launch_ln384_rows_i8) as a launch of its own
+    int defer_ln = 0;
 };
 
 struct EmbedArgs {
@@ -172,12 +167,8 @@ bool qkv_attention_pack_pays(int n_seqs, int n_tiles);
 // of the kernel's QKV weight copy (runtime.cpp), chosen per context at load;
 // 0: the producer / consumer kernel (head dim 32, n_embd 384; plain tile order).
 bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw);
-// n_blocks: tiles (a.tiles) or sentences (a.tiles == null).  o (ntw 0 only):
-// the O projection + residual + LayerNorm runs inside the same kernel after the
-// attention (the O tail), with the int8 O weights o->Wi, bitwise the separate
-// i8 EPI_LN launch (launch_gemm_i8) on a.ctx; o->X / o->out_act: workspace bases.
-hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s,
-                                const GemmArgs *o = nullptr);
+// n_blocks: tiles (a.tiles) or sentences (a.tiles == null)
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s);
 // Small batches, Q4_0 at n_embd 384 / head dim 32, every sentence <= 128 tokens:
 // the int8 QKV of one head and its attention in one workgroup per (head,
 // sentence), bitwise the unfused pair (kernels.hip qkv_attention_small_kernel).
@@ -186,10 +177,6 @@ hipError_t launch_qkv_attention_small(const GemmArgs &g, const AttnArgs &a, int 
 // out_row (optional): output row of each sentence (default: its batch index)
 hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E, float *out, hipStream_t s,
                        const int32_t *out_row = nullptr);
-// the same pooling of LN(X) (LayerNorm on read of the last layer's FFN-down
-// residual sums, E = 384: bitwise launch_pool after the LayerNorm pass)
-hipError_t launch_pool_ln(const float *X, const int32_t *offsets, int n_seqs, int E, const float *ln_w,
-                          const float *ln_b, float eps, float *out, hipStream_t s, const int32_t *out_row = nullptr);
 // dst = the batch's token ids with sentence i taken from sentence perm[i]
 hipError_t launch_gather_tokens(const int32_t *src, const int32_t *src_off, const int32_t *perm, const int32_t *dst_off,
                                 int32_t *dst, int n_seqs, hipStream_t s);
@@ -213,9 +200,6 @@ hipError_t launch_gemm_i8(int wtype, int epi, const GemmArgs &a, int Mpad, hipSt
 // the same GEMMs (bitwise) in 32-row tiles for small batches (EPI_LN: residual
 // kernel + a LayerNorm kernel in i8_ln384_kernel's reduction order)
 hipError_t launch_gemm_i8_small(int wtype, int epi, const GemmArgs &a, int Mpad, hipStream_t s);
-// whether launch_gemm_i8_small takes LayerNorm on read (GemmArgs ln_in /
-// defer_ln) at this size: Q4_0, the K-split kernels (Mpad <= their row bound)
-bool i8_small_ln_on_read(int wtype, int Mpad);
 // the LayerNorm pass after a small EPI_LN GEMM launched with defer_ln
 // (i8_ln384_rows_kernel: X = LN(X) in i8_ln384_kernel's order, + its Q8 form)
 hipError_t launch_ln384_rows_i8(int wtype, const GemmArgs &a, int Mpad, hipStream_t s);

@@ -1297,18 +1297,11 @@ __global__ __launch_bounds__(256) void attention_short_kernel(AttnArgs a, int he
 #define QKVA_SMALL 1
 #endif
 
-// LNP (LayerNorm on read, GemmArgs ln_in): the sentence's A rows are Q8(LN(g.X))
-// made here (ln384_rows_to_lds, bitwise the LayerNorm pass + Q8 store), the
-// head-0 workgroup writing the f32 LN output to g.Xln.
-template <bool LNP>
 __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, AttnArgs a) {
     constexpr int D = 32, E = 384, NKB = E / 32, NK = 128, KST = D + 8, VST = NK + 4;
     __shared__ __attribute__((aligned(16))) _Float16 Qh[NK * KST], Ql[NK * KST], Kh[NK * KST], Kl[NK * KST];
     __shared__ __attribute__((aligned(16))) _Float16 Vh[D * VST], Vl[D * VST];
     __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
-    __shared__ __attribute__((aligned(16))) int8_t aq[LNP ? NK * E : 16];
-    __shared__ uint16_t ad[LNP ? NK * NKB : 8];
-    __shared__ double lpart[LNP ? 48 * 2 * 12 : 1];
     const int h = blockIdx.x, s = blockIdx.y;
     const int beg = a.offsets[s], n = a.offsets[s + 1] - beg;
     if (n > NK || n <= 0 || g.K != E || a.E != E) return;
@@ -1316,10 +1309,6 @@ __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, At
     const int nt = (n + 31) >> 5;
     const int epos = a.expt.pos_n, eneg = a.expt.neg_n;
     for (int i = tid; i < a.expt.n_pad / 8; i += 768) ((uint4 *)etab)[i] = ((const uint4 *)a.expt.compact)[i];
-    if constexpr (LNP) {  // rows beg .. beg + 32 nt - 1 (past the sentence: masked keys, never stored)
-        ln384_rows_to_lds<2>(g.X, beg, 32 * nt, n, g.ln_w, g.ln_b, g.eps, aq, ad, h == 0 ? g.Xln : nullptr, lpart);
-        __syncthreads();
-    }
 
     if (wv < 3 * nt) {
         const int rt = wv / 3, part = wv - 3 * rt, ft0 = 3 * h + part;  // head-major f-tile of Q | K | V
@@ -1331,15 +1320,9 @@ __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, At
         auto load = [&](int b) {
             const int sl = b % RING;
             wq[sl] = i8_wq(g.Wi, NKB, ft0, b);
+            xa[sl] = *(const int4v *)((const int8_t *)g.A.q + row * E + 32 * b + 16 * hh);
             dw[sl] = ((const uint16_t *)g.Wi.dh)[(((int64_t)ft0 * (NKB >> 2) + (b >> 2)) * 32 + r) * 4 + (b & 3)];
-            if constexpr (LNP) {
-                const int lr = 32 * rt + r;
-                xa[sl] = *(const int4v *)(aq + lr * E + 32 * b + 16 * hh);
-                da[sl] = ad[lr * NKB + b];
-            } else {
-                xa[sl] = *(const int4v *)((const int8_t *)g.A.q + row * E + 32 * b + 16 * hh);
-                da[sl] = ((const uint16_t *)g.A.d)[row * NKB + b];
-            }
+            da[sl] = ((const uint16_t *)g.A.d)[row * NKB + b];
         };
 #pragma unroll
         for (int b = 0; b < RING; b++) load(b);
@@ -1446,12 +1429,7 @@ __global__ __launch_bounds__(768) void qkv_attention_small_kernel(GemmArgs g, At
 
 hipError_t launch_qkv_attention_small(const GemmArgs &g, const AttnArgs &a, int n_seqs, hipStream_t s) {
     if (!QKVA_SMALL || g.K != 384 || a.E != 384 || a.H * 32 != a.E || n_seqs <= 0) return hipErrorNotSupported;
-    if (g.ln_in) {
-        if (!g.Xln) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(qkv_attention_small_kernel<true>, dim3(a.H, n_seqs), dim3(768), 0, s, g, a);
-    } else {
-        hipLaunchKernelGGL(qkv_attention_small_kernel<false>, dim3(a.H, n_seqs), dim3(768), 0, s, g, a);
-    }
+    hipLaunchKernelGGL(qkv_attention_small_kernel, dim3(a.H, n_seqs), dim3(768), 0, s, g, a);
     return hipGetLastError();
 }
 
@@ -1747,10 +1725,6 @@ __global__ __launch_bounds__(QKVA_NW * 64) void qkv_attention_kernel(GemmArgs g,
 // tiles; the tiles hold the next head).  LDS: the panel (58 KB), one head's
 // tiles (57 KB), the exp table (40 KB).
 constexpr int QKPC_NP = 6, QKPC_NW = 10;  // producer waves, all waves
-constexpr int QKPC_NW_OT = 12;            // all waves with the O tail (OT)
-#ifndef QKPC_OT_AHEAD
-#define QKPC_OT_AHEAD 3  // O tail: weight blocks in flight (i8_core.h I8ResRing)
-#endif
 #ifndef QKPC_CPRIO
 #define QKPC_CPRIO 0  // A/B: static issue priority of the consumer waves (round 4: 0, 1 and 2 within noise)
 #endif
@@ -1758,29 +1732,15 @@ constexpr int QKPC_NW_OT = 12;            // all waves with the O tail (OT)
 #define QKPC_AHEAD 2  // the producers' weight blocks in flight (i8_core.h I8ResRing)
 #endif
 
-// OT (the O tail): after the last head the workgroup's 12 waves run the O
-// projection + residual + LayerNorm of the tile's rows (bert.cpp:944-962) on
-// the int8 MFMA, from the context the consumers stored (a.ctx, read back into
-// the panel's LDS in 64-row halves): og is the O GemmArgs of i8_ln384_kernel
-// (og.Wi the int8 O weights; og.X / og.out_act the workspace bases), and the
-// main loop and LayerNorm are that kernel's (i8_resident_mainloop /
-// i8_ln384_epilogue), so X and Xa come out bitwise as from the separate
-// gemm_o_ln launch.  Waves 10 and 11 only join the periods' barriers.  The
-// residual half-tile (64 x 384 f32, 96 KiB) is staged by LDS-DMA into the
-// space of the attention tiles and the exp table; rows >= n are computed but
-// never stored.
-template <bool PK, bool OT>
-__global__ __launch_bounds__((OT ? QKPC_NW_OT : QKPC_NW) * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a,
-                                                                                          GemmArgs og) {
-    constexpr int WT = W_Q4_0, D = 32, NP = QKPC_NP, NW = OT ? QKPC_NW_OT : QKPC_NW, BM = 128, NT = NW * 64;
+template <bool PK>
+__global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs g, AttnArgs a) {
+    constexpr int WT = W_Q4_0, D = 32, NP = QKPC_NP, NW = QKPC_NW, BM = 128, NT = NW * 64;
     constexpr int NK = 128, KST = D + 8, VST = NK + 4, E = 384, NKB = E / 32;
     using C = I8Chunk<BM, false>;
     constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
     __shared__ __attribute__((aligned(16))) char apanel[(E / I8_KC) * C::BYTES];
-    // OT: the tiles and the exp table in one array (the tail's residual half-tile spans both)
-    __shared__ __attribute__((aligned(16))) char tiles[OT ? SLOT + 2 * EXP_TABLE_LDS : SLOT];
-    __shared__ __attribute__((aligned(16))) uint16_t etab_own[OT ? 8 : EXP_TABLE_LDS];
-    uint16_t *etab = OT ? (uint16_t *)(tiles + SLOT) : etab_own;
+    __shared__ __attribute__((aligned(16))) char tiles[SLOT];
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     __shared__ int qtab[PK ? 4 : 1][4];     // query block -> {first tile row of its sentence, length, first query, vs}
     __shared__ uint8_t vslot[PK ? NK : 1];  // tile row -> V^T key slot
     const int s0 = PK ? a.tiles[2 * blockIdx.x] : (int)blockIdx.x;
@@ -1891,7 +1851,7 @@ __global__ __launch_bounds__((OT ? QKPC_NW_OT : QKPC_NW) * 64) void qkv_attentio
             __syncthreads();  // Y: head p's tiles are complete
             STAMP(p + 1, 0, NW);
         }
-    } else if (!OT || wv < NP + 4) {
+    } else {
         // ---- consumer: query block qb of head p - 1 (32 queries of one sentence)
         const int qb = wv - NP;
         int lim = n - 4 * hh;  // key mask limit for lane half hh (opaque: not hoisted into SGPRs)
@@ -1989,102 +1949,18 @@ __global__ __launch_bounds__((OT ? QKPC_NW_OT : QKPC_NW) * 64) void qkv_attentio
             __syncthreads();  // Y
             STAMP(p + 1, 0, NW);
         }
-    } else {
-        // ---- OT: waves 10, 11 wait through the periods
-        for (int p = 0; p <= H; p++) {
-            __syncthreads();  // X
-            __syncthreads();  // Y
-        }
-    }
-    if constexpr (OT) {
-        // ---- O tail: X = LN((b_o + W_o.ctx) + X) over the tile's rows in two 64-row
-        // halves; wave w: O f-tile w (features 32 w ..) of both 32-row t-tiles
-        constexpr int HB = 64, NCOL = 384, PIECES = HB * NCOL / 4 / NT;  // 1 KiB residual pieces per wave
-        using C64 = I8Chunk<HB, false>;
-        static_assert(3 * C64::BYTES + 2 * 12 * HB * 8 <= (int)sizeof(apanel), "context half-panel + red");
-        static_assert(HB * NCOL * 4 <= SLOT + 2 * EXP_TABLE_LDS, "residual half-tile");
-        static_assert(PIECES * NT * 4 == HB * NCOL, "whole pieces per wave");
-        char *cpanel = apanel;
-        double(*red)[12][64] = (double(*)[12][64])(apanel + 3 * C64::BYTES);
-        float *xs = (float *)tiles;
-        auto piece_off = [&](int k, int &j0, int &prow) {  // i8_ln384_kernel's piece map
-            j0 = 64 * (PIECES * wv + k);
-            const int j = j0 + lane, rr = j / 96, cs = j - 96 * rr;
-            prow = rr;
-            return rr * NCOL + 4 * (cs ^ (rr & 15));
-        };
-        auto dma_in = [&](const float *xt, int k) {
-            int j0, prow;
-            const int off = piece_off(k, j0, prow);
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(xt + off),
-                                             (__attribute__((address_space(3))) void *)(xs + 4 * j0), 16, 0, 0);
-        };
-        auto store_out = [&](float *xt, int k, int nvalid) {
-            int j0, prow;
-            const int off = piece_off(k, j0, prow);
-            if (prow < nvalid) *(float4v *)(xt + off) = *(const float4v *)(xs + 4 * (j0 + lane));
-        };
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the consumers' context stores
-        __syncthreads();
-        I8ResRing<WT, 1, QKPC_OT_AHEAD> oring;
-        oring.start(og, wv);
-        const int nh = n > HB ? 2 : 1;
-        for (int hf = 0; hf < nh; hf++) {
-            const int64_t m0 = beg + HB * hf;
-            const int nvalid = n - HB * hf;
-            {   // context rows m0 .. m0 + 63 -> cpanel (I8Chunk<64> layout): one (row, block) per thread
-                static_assert(HB * NKB == NT, "one context item per thread");
-                const int row = tid / NKB, b = tid - row * NKB, c = b >> 2, bb = b & 3;
-                const int4v *src = (const int4v *)((const int8_t *)a.ctx.q + (m0 + row) * E + 32 * b);
-                char *buf = cpanel + c * C64::BYTES;
-                int4v *dst = (int4v *)(buf + row * I8_LDQ + 32 * bb);
-                dst[0] = src[0];
-                dst[1] = src[1];
-                ((uint16_t *)(buf + C64::QB))[bb * HB + row] = ((const uint16_t *)a.ctx.d)[(m0 + row) * NKB + b];
-            }
-            __syncthreads();
-            // the half's residual arrives by LDS-DMA piece by piece during its main
-            // loop; in the second half each piece first drains the first half's LN output
-            const float *xin = og.X + m0 * NCOL;
-            float *xprev = og.X + (m0 - HB) * NCOL;
-            auto hook = [&](int c, int nch) {
-                const int ppc = (PIECES + nch - 1) / nch, k1 = min(PIECES, (c + 1) * ppc);
-#pragma unroll 1
-                for (int k = c * ppc; k < k1; k++) {
-                    if (hf > 0) store_out(xprev, k, HB);
-                    dma_in(xin, k);
-                }
-            };
-            float16v acc[1][2];
-            i8_resident_mainloop<WT, HB, 1, 2, QKPC_OT_AHEAD>(og, cpanel, wv, 0, acc, oring, hf + 1 < nh ? wv : -1, hook);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces have landed
-            __syncthreads();                                   // ... and every other wave's
-            i8_ln384_epilogue<WT, true>(acc, xs, red, og, m0, nvalid, 0);
-            __syncthreads();  // the LN output is in xs; the context half-panel is free
-        }
-        {   // the last half's LN output
-            const int64_t m0 = beg + HB * (nh - 1);
-#pragma unroll 1
-            for (int k = 0; k < PIECES; k++) store_out(og.X + m0 * NCOL, k, n - HB * (nh - 1));
-        }
     }
 }
 
 template <int WT, int D>
-static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s,
-                              const GemmArgs *o) {
+static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s) {
     const bool pk = a.tiles != nullptr;
     if constexpr (D == 32 && WT == W_Q4_0) {
         if (ntw == 0) {  // producer / consumer waves (qkv_attention_pc_kernel; g.Wi: int8 QKV weights)
-            const GemmArgs oa = o ? *o : GemmArgs{};
-            if (o && pk)
-                hipLaunchKernelGGL((qkv_attention_pc_kernel<true, true>), dim3(n_blocks), dim3(QKPC_NW_OT * 64), 0, s, g, a, oa);
-            else if (o)
-                hipLaunchKernelGGL((qkv_attention_pc_kernel<false, true>), dim3(n_blocks), dim3(QKPC_NW_OT * 64), 0, s, g, a, oa);
-            else if (pk)
-                hipLaunchKernelGGL((qkv_attention_pc_kernel<true, false>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a, oa);
+            if (pk)
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<true>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a);
             else
-                hipLaunchKernelGGL((qkv_attention_pc_kernel<false, false>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a, oa);
+                hipLaunchKernelGGL((qkv_attention_pc_kernel<false>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a);
             return hipGetLastError();
         }
     }
@@ -2103,11 +1979,10 @@ static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks,
 }
 
 template <int WT>
-static hipError_t qkv_attn_w(const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s,
-                              const GemmArgs *o) {
+static hipError_t qkv_attn_w(const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s) {
     switch (a.H > 0 ? a.E / a.H : 0) {
-        case 32: return qkv_attn_t<WT, 32>(g, a, n_blocks, ntw, s, o);
-        case 64: return qkv_attn_t<WT, 64>(g, a, n_blocks, ntw, s, o);
+        case 32: return qkv_attn_t<WT, 32>(g, a, n_blocks, ntw, s);
+        case 64: return qkv_attn_t<WT, 64>(g, a, n_blocks, ntw, s);
     }
     return hipErrorInvalidValue;
 }
@@ -2156,14 +2031,12 @@ bool qkv_attention_supported(int wtype, int E, int H, int max_len, int ntw) {
            wtype != W_F32;
 }
 
-hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s,
-                                const GemmArgs *o) {
+hipError_t launch_qkv_attention(int wtype, const GemmArgs &g, const AttnArgs &a, int n_blocks, int ntw, hipStream_t s) {
     if (!qkv_attention_supported(wtype, a.E, a.H, 0, ntw)) return hipErrorInvalidValue;
-    if (o && (ntw != 0 || wtype != W_Q4_0 || o->K != a.E || o->N != a.E)) return hipErrorInvalidValue;  // the O tail: pc kernel only
     switch (wtype) {
-        case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, ntw, s, o);
-        case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, ntw, s, o);
-        case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, ntw, s, o);
+        case W_F16: return qkv_attn_w<W_F16>(g, a, n_blocks, ntw, s);
+        case W_Q4_0: return qkv_attn_w<W_Q4_0>(g, a, n_blocks, ntw, s);
+        case W_Q4_1: return qkv_attn_w<W_Q4_1>(g, a, n_blocks, ntw, s);
     }
     return hipErrorInvalidValue;
 }
@@ -2627,58 +2500,6 @@ hipError_t launch_pool(const float *X, const int32_t *offsets, int n_seqs, int E
                        const int32_t *out_row) {
     if (E > 1024) return hipErrorInvalidValue;
     hipLaunchKernelGGL(pool_l2_kernel, dim3(n_seqs), dim3(256), 0, s, X, offsets, E, out, out_row);
-    return hipGetLastError();
-}
-
-// pool_l2_kernel over LN(X) (LayerNorm on read of the last layer's residual
-// sums, E = 384): the sentence's rows in chunks of 32, each normalised by one
-// wave into LDS (ln384_row_wave: bitwise the LayerNorm pass), then pooled in
-// row order exactly as pool_l2_kernel.
-__global__ __launch_bounds__(1024) void pool_l2_ln_kernel(const float *X, const int32_t *offsets, const float *ln_w,
-                                                          const float *ln_b, float eps, float *out,
-                                                          const int32_t *out_row) {
-    constexpr int E = 384, CH = 32;  // 16 waves: one 32-row chunk per pass (two rows a wave)
-    __shared__ __attribute__((aligned(16))) float ys[CH * E];
-    __shared__ __attribute__((aligned(16))) int8_t aq[CH * E];  // (the Q8 form: unused here)
-    __shared__ uint16_t ad[CH * 12];
-    __shared__ double lpart[48 * 16];
-    __shared__ double red[16];
-    const int s = blockIdx.x, tid = threadIdx.x, c = 4 * tid;
-    const int beg = offsets[s], n = offsets[s + 1] - beg;
-    const float invN = 1.0f / n;
-    float4v acc = {0.f, 0.f, 0.f, 0.f};
-    for (int t0 = 0; t0 < n; t0 += CH) {
-        const int nc = min(CH, n - t0);
-        ln384_rows_to_lds<1>(X, (int64_t)beg + t0, nc, 0, ln_w, ln_b, eps, aq, ad, nullptr, lpart, ys);
-        __syncthreads();
-        if (c < E) {
-            for (int t = 0; t < nc; t++) {
-                const float4v x = *(const float4v *)(ys + t * E + c);
-#pragma unroll
-                for (int j = 0; j < 4; j++) acc[j] = fmaf(x[j], invN, acc[j]);
-            }
-        }
-        __syncthreads();
-    }
-    // pool_l2_kernel's norm: its 96 active threads sit in its first two waves
-    // (lanes 0-63, 64-95); the others add zeros, so red[0] + red[1] (+ 0 + 0) is its sum
-    double ss = 0.0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) ss += (double)(acc[j] * acc[j]);
-    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-    if ((tid & 63) == 0) red[tid >> 6] = ss;
-    __syncthreads();
-    const double tot = red[0] + red[1] + red[2] + red[3];
-    const float len = sqrtf((float)tot);
-    const float r = 1.0f / len;
-    const int64_t orow = out_row ? out_row[s] : s;
-    if (c < E) *(float4v *)(out + orow * E + c) = float4v{acc[0] * r, acc[1] * r, acc[2] * r, acc[3] * r};
-}
-
-hipError_t launch_pool_ln(const float *X, const int32_t *offsets, int n_seqs, int E, const float *ln_w,
-                          const float *ln_b, float eps, float *out, hipStream_t s, const int32_t *out_row) {
-    if (E != 384) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pool_l2_ln_kernel, dim3(n_seqs), dim3(1024), 0, s, X, offsets, ln_w, ln_b, eps, out, out_row);
     return hipGetLastError();
 }
 

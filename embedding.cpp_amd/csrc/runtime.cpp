@@ -187,10 +187,6 @@ struct Workspace {
     int64_t cap_rows = 0;   // padded rows
     int64_t cap_seqs = 0;
     float *X = nullptr, *out = nullptr;
-    // LayerNorm on read (small batches): the other residual buffer — X and P
-    // take turns holding a layer's pre-LN sums and its LN output (run_layer);
-    // LN_READ_ROWS + GEMM_BM rows (spare rows zero)
-    float *P = nullptr;
     uint16_t *qk_hi = nullptr, *qk_lo = nullptr, *vt_hi = nullptr, *vt_lo = nullptr;  // fp16: kernels.h GemmArgs EPI_QKV
     ActPtr Xa, Ca, Ua;
     int32_t *tok = nullptr, *off = nullptr, *rowpos = nullptr;
@@ -309,22 +305,6 @@ struct bert_ctx {
     // of f32 rows: MiniLM Q4_0's table 47 -> 6.6 MB, embed_ln 96-98 -> 90-92 us
     // on the headline batch (round 6, profiles/r06_embraw_ab.txt), bitwise equal
     bool emb_raw = true;
-    // the O projection + residual + LayerNorm inside the producer / consumer
-    // kernel after each sentence's attention (kernels.hip qkv_attention_pc_kernel
-    // OT), where that kernel runs and O is on the int8 GEMM: one launch and the
-    // context's HBM round trip fewer per layer, bitwise the separate i8 O + LN
-    // launch (option o_tail).  Default 0: the tail adds 158-160 us to the
-    // fused kernel against 147-151 us for the separate launch (round 6,
-    // profiles/r06_otail_ab.txt): serial after the attention, it has nothing
-    // to overlap with inside the one workgroup per CU
-    bool o_tail = false;
-    // LayerNorm on read for small batches (Q4_0 at n_embd 384, every projection
-    // int8, <= 512 padded rows): the O and FFN-down LayerNorms run in the
-    // prologue of the kernel that reads their output (FFN-up, the next layer's
-    // QKV, the pooling) instead of as a pass of their own — two launches fewer
-    // per layer, bitwise the same (option ln_read).  Default 0: one sentence
-    // measured 264-283 us against 238-250 (profiles/r06_lnread_ab.txt)
-    bool ln_read = false;
     uint64_t opt_gen = 0;  // bumped by every option change (captured graphs are dropped)
     // bert_encode_batch: slices evaluated at once per device (lanes), >= 1,
     // and consecutive slices a lane evaluates as one ragged batch (merge, >= 1),
@@ -595,10 +575,6 @@ std::vector<const uint8_t *> rows_of(const GGUFTensor *t) {
 
 // activation format (ggml's vec_dot_type of the weights, kernels.h WType) of
 // a row of K values: element / block-scale bytes
-// LayerNorm on read covers batches of at most this many padded rows (the
-// K-split small kernels' bound, i8_small_ln_on_read)
-constexpr int64_t LN_READ_ROWS = 512;
-
 size_t act_row_bytes(int at, int64_t K) { return (size_t)K * (at == W_F32 ? 4 : at == W_F16 ? 2 : 1); }
 size_t act_scale_bytes(int at) { return at == W_Q4_0 ? 2 : at == W_Q4_1 ? 4 : 0; }
 
@@ -634,27 +610,23 @@ bool ensure_workspace(bert_ctx *ctx, Lane &ln, int64_t Mpad, int64_t n_seqs, hip
     // until every allocation below has succeeded the workspace is empty
     // (a failed grow must not leave capacities that point at freed memory)
     w.cap_rows = w.cap_seqs = 0;
-    w.X = w.out = w.P = nullptr;
+    w.X = w.out = nullptr;
     w.qk_hi = w.qk_lo = w.vt_hi = w.vt_lo = nullptr;
     w.Xa = w.Ca = w.Ua = ActPtr{};
     w.tok = w.off = w.rowpos = w.tiles = w.perm = nullptr;
     const int64_t E = ctx->hp.n_embd, I = ctx->hp.n_intermediate;
     const int at = ctx->wtype;
-    // X too carries GEMM_BM spare rows: the O tail stages 64-row residual halves
-    // from each sentence's first token (rows past the sentence are never stored)
-    if (!dmalloc(w.allocs, &w.X, (size_t)(rows + GEMM_BM) * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
+    if (!dmalloc(w.allocs, &w.X, (size_t)rows * E * 4) || !dmalloc(w.allocs, &w.qk_hi, (size_t)rows * 2 * E * 2) ||
         !dmalloc(w.allocs, &w.qk_lo, (size_t)rows * 2 * E * 2) || !dmalloc(w.allocs, &w.vt_hi, (size_t)rows * E * 2) ||
         !dmalloc(w.allocs, &w.vt_lo, (size_t)rows * E * 2) ||
         !alloc_act(w.allocs, w.Xa, ctx->wtype, rows, E, st) || !alloc_act(w.allocs, w.Ca, at, rows, E, st) ||
         !alloc_act(w.allocs, w.Ua, at, rows, I, st) || !dmalloc(w.allocs, &w.out, (size_t)seqs * E * 4) ||
         !dmalloc(w.allocs, &w.tok, (size_t)rows * 4) || !dmalloc(w.allocs, &w.off, (size_t)(seqs + 1) * 4) ||
         !dmalloc(w.allocs, &w.rowpos, (size_t)rows * 4) || !dmalloc(w.allocs, &w.tiles, (size_t)seqs * 2 * 4) ||
-        !dmalloc(w.allocs, &w.perm, (size_t)seqs * 4) ||
-        !dmalloc(w.allocs, &w.P, (size_t)(LN_READ_ROWS + GEMM_BM) * E * 4))
+        !dmalloc(w.allocs, &w.perm, (size_t)seqs * 4))
         return false;
-    HIP_OK(hipMemsetAsync(w.P, 0, (size_t)(LN_READ_ROWS + GEMM_BM) * E * 4, st));
     // padding rows must hold finite values: zero everything once
-    HIP_OK(hipMemsetAsync(w.X, 0, (size_t)(rows + GEMM_BM) * E * 4, st));
+    HIP_OK(hipMemsetAsync(w.X, 0, (size_t)rows * E * 4, st));
     HIP_OK(hipMemsetAsync(w.qk_hi, 0, (size_t)rows * 2 * E * 2, st));
     HIP_OK(hipMemsetAsync(w.qk_lo, 0, (size_t)rows * 2 * E * 2, st));
     HIP_OK(hipMemsetAsync(w.vt_hi, 0, (size_t)rows * E * 2, st));
@@ -735,9 +707,9 @@ bool ws_release(Lane &ln, hipStream_t st) {
 // the kernel like ggml's vec_dot).  Default: FFN-up (faster than the
 // split-fp16 GEMM) and FFN-down (as fast on full batches, faster on ragged
 // ones) where its LayerNorm is fused (n_embd 384); the O projection too for
-// Q4_0 at n_embd 384 (its small-batch tiles beat the split-fp16 ones, and the
-// producer / consumer kernel runs it as its O tail: round 6), elsewhere it
-// stays on the split-fp16 GEMM.  `v` (load option "i8", env
+// Q4_0 at n_embd 384 (batch within noise of the split-fp16 GEMM, one sentence
+// 15-20 us faster: its 32-row int8 tiles stream a quarter of the bytes; round
+// 6), elsewhere it stays on the split-fp16 GEMM.  `v` (load option "i8", env
 // BERT_AMD_I8): "0" none, "1" / "all" all three, or a list of up, o, down
 // separated by '+' or ','; empty: the default.
 void i8_select(bert_ctx *ctx, const std::string &spec) {
@@ -784,13 +756,9 @@ void i8_select(bert_ctx *ctx, const std::string &spec) {
 // i8_ln384 FFN-down 366 -> 443 us)
 static bool q41bf_for(int opt, int epi) { return opt > 0 || (opt < 0 && epi != EPI_LN); }
 
-// ln_read (LayerNorm on read, run_pipeline; one row group): layer il's input is
-// LN2_{il-1}(P) for il > 0 (the QKV kernel normalises its A rows and writes the
-// LN output to X); O leaves its pre-LN sums in X, FFN-up normalises them on
-// read (LN output -> P), FFN-down leaves its pre-LN sums in P.
 bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_t rows, const int32_t *d_off, int nseq,
                const int32_t *d_tiles, int ntiles, int max_len, bool fused_qkv_attn, bool ln_fused, ActPtr Xa,
-               ActPtr Ca, ActPtr Ua, float *X, hipStream_t st, bool ln_read = false) {
+               ActPtr Ca, ActPtr Ua, float *X, hipStream_t st) {
     const HParams &hp = ctx->hp;
     Workspace &w = ln.ws;
     const int E = hp.n_embd, I = hp.n_intermediate, H = hp.n_head, D = E / H, wt = ctx->wtype;
@@ -821,14 +789,6 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         q.vt_hi = w.vt_hi;
         q.vt_lo = w.vt_lo;
         q.ldv = w.cap_rows;
-        if (ln_read && il > 0) {  // A = Q8(LN2_{il-1}(P)); the LN output -> X (O's residual)
-            q.ln_in = 1;
-            q.X = w.P;
-            q.ln_w = R.L[il - 1].ln2_w;
-            q.ln_b = R.L[il - 1].ln2_b;
-            q.eps = hp.eps;
-            q.Xln = X;
-        }
         AttnArgs aa;
         aa.qk_hi = w.qk_hi;
         aa.qk_lo = w.qk_lo;
@@ -841,34 +801,12 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         aa.scale = 1.0f / sqrtf((float)D);
         aa.expt = half_table(R.exp_tab, R.exp_compact, tables().exp_c);
         aa.ctx = w.Ca;
-        GemmArgs o;
-        o.A = Ca;
-        o.K = E;
-        o.W = L.o;
-        o.N = E;
-        o.bias = L.b_o;
-        o.X = X;
-        o.out_act = Xa;
-        o.ln_w = L.ln1_w;
-        o.ln_b = L.ln1_b;
-        o.eps = hp.eps;
-        // small batches: the int8 O + LN is the K-split residual GEMM, then the
-        // LayerNorm pass as a launch of its own — or none: FFN-up normalises X on read
-        o.defer_ln = small;
-        if (ctx->i8_o) o.Wi = L.o8;
-        // the O tail (ctx->o_tail): the fused kernel addresses rows absolutely, so
-        // its O arguments get the workspace bases
-        const bool o_tail = fused_qkv_attn && ctx->o_tail && ctx->i8_o && ctx->qkva_ntw == 0 && wt == W_Q4_0 && E == 384;
-        GemmArgs ot = o;
-        ot.A = w.Ca;
-        ot.X = w.X;
-        ot.out_act = w.Xa;
         if (fused_qkv_attn) {
             GemmArgs qf = q;
             qf.W = L.qkv_plain;
             aa.tiles = ntiles < nseq ? d_tiles : nullptr;  // no tile holds two sentences: plain kernel
             qf.Wi = L.qkv8;  // (qkva_ntw 0)
-            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st, o_tail ? &ot : nullptr));
+            LAUNCH_OK("qkv_attention", launch_qkv_attention(wt, qf, aa, ntiles, ctx->qkva_ntw, st));
         } else if (ctx->i8_qkv && ctx->small_qkva && !ctx->unfused && small && wt == W_Q4_0 && E == 384 && D == 32 &&
                    max_len <= QKVA_SMALL_MAX_LEN && rows <= QKVA_SMALL_ROWS) {
             // one sentence (the server's path): the head's QKV and attention in one kernel
@@ -882,13 +820,25 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             LAUNCH_OK("gemm_qkv", launch_gemm(wt, EPI_QKV, 0, q, (int)rows, st));
             LAUNCH_OK("attention", launch_attention(wt, D, aa, nseq, max_len, st));
         }
-        if (o_tail) {
-            // O + LN ran inside the fused kernel (its O tail)
-        } else if (ctx->i8_o) {
+        GemmArgs o;
+        o.A = Ca;
+        o.K = E;
+        o.W = L.o;
+        o.N = E;
+        o.bias = L.b_o;
+        o.X = X;
+        o.out_act = Xa;
+        o.ln_w = L.ln1_w;
+        o.ln_b = L.ln1_b;
+        o.eps = hp.eps;
+        // small batches: the int8 O + LN is the 32-row residual GEMM, then the
+        // LayerNorm pass as a launch of its own (counted as one in the profile)
+        o.defer_ln = small;
+        if (ctx->i8_o) {
             o.Wi = L.o8;
             if (E == 384) {
                 LAUNCH_OK("gemm_o_ln", gemm_i8(EPI_LN, o));
-                if (small && !ln_read) LAUNCH_OK("ln", launch_ln384_rows_i8(wt8(EPI_LN), o, (int)rows, st));
+                if (small) LAUNCH_OK("ln", launch_ln384_rows_i8(wt8(EPI_LN), o, (int)rows, st));
             } else {
                 LAUNCH_OK("gemm_o_ln", gemm_i8(EPI_RESID, o));
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln1_w, L.ln1_b, hp.eps, Xa, st));
@@ -910,14 +860,6 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         u.gelu = half_table(R.gelu_tab, R.gelu_compact, tables().gelu_c);
         u.gelu.n_pad = (int)tables().gelu_pair.size();  // the pair view (kernels.hip gelu_lookup)
         u.gelu.cap = tables().gelu_cap;
-        if (ln_read) {  // A = Q8(LN1(X)); the LN output -> P (FFN-down's residual)
-            u.ln_in = 1;
-            u.X = X;
-            u.ln_w = L.ln1_w;
-            u.ln_b = L.ln1_b;
-            u.eps = hp.eps;
-            u.Xln = w.P;
-        }
         GemmArgs dn;
         dn.A = Ua;
         dn.K = I;
@@ -929,8 +871,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         dn.ln_w = L.ln2_w;
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
-        dn.defer_ln = small;  // (as O: the LayerNorm pass of its own, or on read)
-        if (ln_read) dn.X = w.P;  // (b + W.u) + LN1 output, in place in P; normalised by the next reader
+        dn.defer_ln = small;  // (as O)
         if (ctx->i8_up) {
             u.Wi = L.up8;
             LAUNCH_OK("gemm_up_gelu", gemm_i8(EPI_GELU_ACT, u));
@@ -942,7 +883,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
             dn.Wi = L.down8;
             if (E == 384) {
                 LAUNCH_OK("gemm_down_ln", gemm_i8(EPI_LN, dn));
-                if (small && !ln_read) LAUNCH_OK("ln", launch_ln384_rows_i8(wt8(EPI_LN), dn, (int)rows, st));
+                if (small) LAUNCH_OK("ln", launch_ln384_rows_i8(wt8(EPI_LN), dn, (int)rows, st));
             } else {
                 LAUNCH_OK("gemm_down_ln", gemm_i8(EPI_RESID, dn));
                 LAUNCH_OK("ln", launch_ln(wt, X, (int)rows, E, L.ln2_w, L.ln2_b, hp.eps, Xa, st));
@@ -1019,10 +960,6 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
     const bool fused_qkv_attn = !ctx->unfused && n_seqs >= ctx->fuse_min && (!ctx->i8_qkv || ctx->qkva_ntw == 0) &&
                                 qkv_attention_supported(wt, E, H, max_len, ctx->qkva_ntw) && !small_short;
 
-    // LayerNorm on read (ctx->ln_read): small batches on the K-split int8 kernels
-    const bool ln_read = ctx->ln_read && wt == W_Q4_0 && E == 384 && E / H == 32 && ctx->i8_qkv && ctx->i8_o &&
-                         ctx->i8_up && ctx->i8_down && !tap && !fused_qkv_attn && Mpad <= ctx->small_rows &&
-                         Mpad <= LN_READ_ROWS && i8_small_ln_on_read(wt, (int)Mpad) && max_len <= GEMM_BM;
     const EmbedArgs ea = embed_args(ctx, R, w, d_tok, d_off, n_seqs, M);
     LAUNCH_OK("embed_ln", launch_embed(ctx->wtype, ea, (int)Mpad, st));
     auto tap_stage = [&](int stage) {
@@ -1120,8 +1057,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
             const Group &gr = G[gi];
             if (!run_layer(ctx, R, ln, il, gr.row0, gr.rows, d_off + gr.seq0, gr.nseq, w.tiles + 2 * gr.seq0, ntl[gi],
                            max_len, fused_qkv_attn, ln_fused, act_rows(w.Xa, wt, gr.row0, E),
-                           act_rows(w.Ca, wt, gr.row0, E), act_rows(w.Ua, wt, gr.row0, I), w.X + gr.row0 * E, gr.s,
-                           ln_read && ng == 1))
+                           act_rows(w.Ca, wt, gr.row0, E), act_rows(w.Ua, wt, gr.row0, I), w.X + gr.row0 * E, gr.s))
                 return false;
         }
         if (!tap_stage(il + 1)) return false;
@@ -1130,12 +1066,7 @@ bool run_pipeline(bert_ctx *ctx, Replica &R, Lane &ln, const int32_t *d_tok, con
         HIP_OK(hipEventRecord(ln.ev_join, ln.stream2));
         HIP_OK(hipStreamWaitEvent(st, ln.ev_join, 0));
     }
-    if (ln_read && ng == 1) {  // the last FFN-down's LayerNorm, on read
-        const DevLayer &Ll = R.L[hp.n_layer - 1];
-        LAUNCH_OK("pool_l2", launch_pool_ln(w.P, d_off, n_seqs, E, Ll.ln2_w, Ll.ln2_b, hp.eps, d_out, st, d_out_row));
-    } else {
-        LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st, d_out_row));
-    }
+    LAUNCH_OK("pool_l2", launch_pool(w.X, d_off, n_seqs, E, d_out, st, d_out_row));
     return true;
 }
 
@@ -1381,10 +1312,6 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         ctx->unfused = value != 0;
     } else if (k == "small_qkva") {
         ctx->small_qkva = value != 0;
-    } else if (k == "o_tail") {
-        ctx->o_tail = value != 0;
-    } else if (k == "ln_read") {
-        ctx->ln_read = value != 0;
     } else if (k == "small_rows" || k == "graph_seqs") {
         if (need(value >= 0, "must be >= 0")) return -2;
         (k == "small_rows" ? ctx->small_rows : ctx->graph_seqs) = value;
@@ -1407,7 +1334,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
     static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows", "graph_seqs",
-                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows", "emb_raw", "o_tail", "ln_read"};
+                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows", "emb_raw"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
         std::string env = "BERT_AMD_" + std::string(k);
@@ -2444,10 +2371,7 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
-        {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw}, {"o_tail", ctx->o_tail}, {"ln_read", ctx->ln_read},
-        // resolved: O + LN inside the producer / consumer kernel (run_layer's o_tail,
-        // for the batches that take that kernel)
-        {"o_tail_active", ctx->o_tail && ctx->i8_o && ctx->qkva_ntw == 0 && ctx->wtype == W_Q4_0 && ctx->hp.n_embd == 384},
+        {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw},
         // resolved: FFN-up / FFN-down on the bf16 scale products (Q4_1 on the int8 GEMMs)
         {"q41bf_qkv", ctx->wtype == W_Q4_1 && ctx->i8_qkv && q41bf_for(ctx->q41bf, EPI_QKV)},
         {"q41bf_o", ctx->wtype == W_Q4_1 && ctx->i8_o && q41bf_for(ctx->q41bf, ctx->hp.n_embd == 384 ? EPI_LN : EPI_RESID)},

@@ -139,12 +139,6 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
                         sentences all have <= 64 tokens (Q4_0, n_embd 384, head
                         dim 32) run each head's int8 QKV and its attention in one
                         kernel (same results; one launch less per layer)
-     "o_tail" 0 | 1     1: where the producer / consumer kernel runs (qkva_ntw
-                        0) and O is on the int8 GEMM, the O projection +
-                        residual + LayerNorm run inside it after each sentence's
-                        attention (same results; one launch less per layer, but
-                        measured slower); 0 (default): the separate O +
-                        LayerNorm launch
      "graph_seqs" n >= 0 host batches of at most n sentences (and fewer than
                         fuse_min) replay a captured HIP graph of their launches
                         (default 0: measured no faster)
@@ -168,9 +162,8 @@ BERT_API int32_t bert_amd_set_option(struct bert_ctx *ctx, const char *key, int3
    and its unfused int8 twin), "q41bf" (the load option: -1 auto, 0, 1) and
    "q41bf_qkv", "q41bf_o", "q41bf_up", "q41bf_down" (1 when that Q4_1
    projection's int8 GEMM takes its scale products on the bf16 MFMA,
-   W_Q4_1B), "o_tail_active" (1 when batches that take the producer /
-   consumer kernel also run their O + LayerNorm in it).  Lets bench.py price
-   each kernel on the arithmetic it runs.  Returns 0, or -2 on an unknown key. */
+   W_Q4_1B).  Lets bench.py price each kernel on the
+   arithmetic it runs.  Returns 0, or -2 on an unknown key. */
 BERT_API int32_t bert_amd_get_option(struct bert_ctx *ctx, const char *key, int32_t *value);
 
 /* How bert_eval_batch splits a batch over n_replicas devices: contiguous

@@ -13,8 +13,7 @@ import bench  # noqa: E402
 import bertlib  # noqa: E402
 
 HP = bertlib.SHAPES["minilm"]
-PC = {"qkva_ntw": 0, "i8_up": 1, "i8_o": 0, "i8_down": 1}  # the Q4_0 MiniLM defaults of rounds 4-5
-PC6 = {"qkva_ntw": 0, "i8_qkv": 1, "i8_up": 1, "i8_o": 1, "i8_down": 1, "o_tail_active": 1}  # round 6
+PC = {"qkva_ntw": 0, "i8_up": 1, "i8_o": 0, "i8_down": 1}  # the Q4_0 MiniLM defaults of rounds 4-5 (O split-fp16)
 
 
 def test_qkv_attention_mixed_price():
@@ -58,21 +57,3 @@ def test_int8_qkv_gemm_priced_by_resolved_choice():
     assert bench.dtype_label("q4_1", off) == "fp16"
     # the pc kernel reports i8_qkv = 1 with qkva_ntw = 0
     assert bench.kernel_parts("gemm_qkv", 8, 128, HP, dict(PC, i8_qkv=1), "q4_0")[0][1] == bench.PEAK_INT8_TOPS
-
-
-def test_o_tail_priced_inside_the_fused_kernel():
-    """Round 6: with the O tail the producer / consumer kernel also runs the O
-    projection (int8) and its LayerNorm: one more int8 part, and its bytes are
-    Xa + the residual X in, X + Xa out (the context never leaves the kernel's
-    workgroup as algorithmic traffic)."""
-    parts = bench.kernel_parts("qkv_attention", 1024, 128, HP, PC6, "q4_0")
-    assert [p for _, p in parts] == [bench.PEAK_INT8_TOPS, bench.PEAK_FP16_TFLOPS, bench.PEAK_INT8_TOPS]
-    M, E = 1024 * 128, HP["n_embd"]
-    assert parts[2][0] == pytest.approx(2.0 * M * E * E)
-    plain = bench.kernel_bytes("qkv_attention", 1024, 128, HP, "q4_0", PC)
-    tail = bench.kernel_bytes("qkv_attention", 1024, 128, HP, "q4_0", PC6)
-    act = 1 + 2 / 32
-    assert tail - plain == pytest.approx(E * E * 18 / 32 + 2 * M * E * 4)
-    assert plain == pytest.approx(2 * M * E * act + 3 * E * E * 18 / 32)
-    assert "O + LN inside the fused" in bench.dtype_note("q4_0", PC6)
-    assert "qkv/o/up/down on int8 MFMA" in bench.dtype_note("q4_0", PC6)

@@ -1052,88 +1052,6 @@ def test_producer_consumer_kernel(model_dir):
 
 
 
-def test_o_tail_bitwise_separate_o_launch(model_dir):
-    """The O tail (option o_tail; default 0, measured slower): where the producer / consumer
-    kernel runs, its 12 waves finish each sentence with the O projection +
-    residual + LayerNorm (int8 O, i8_ln384_kernel's main loop and LayerNorm)
-    instead of a separate gemm_o_ln launch.  The residual stream X and its Q8
-    form after every layer, and the embeddings, are bitwise those of the
-    separate launch: sentences of 2..128 tokens (one or two 64-row halves),
-    packed tiles of short sentences, full 128-token sentences, and a batch whose
-    last sentence ends off the 128-row padding (the tail's halves read rows past
-    it, never store them).  Reference: bert.cpp:944-962."""
-    p, _ = get_model(model_dir, "minilm", "q4_0")
-    m = bertlib.BertModel(p)
-    try:
-        assert m.get_option("i8_o") == 1 and m.get_option("qkva_ntw") == 0
-        assert m.get_option("o_tail") == 0 and m.get_option("o_tail_active") == 0
-        m.set_option("o_tail", 1)
-        assert m.get_option("o_tail_active") == 1
-        rng = np.random.default_rng(77)
-        batches = [[[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in rng.integers(2, 129, 300)],
-                   [[101] + rng.integers(1000, 30522, int(n) - 2).tolist() + [102] for n in rng.integers(2, 41, 500)],
-                   [sentence(900 + i, 128, 30522) for i in range(64)],
-                   [sentence(1000 + i, 65 + i, 30522) for i in range(50)] + [sentence(7, 3, 30522)]]
-        for bi, toks in enumerate(batches):
-            got = {}
-            for ot in (1, 0):
-                m.set_option("o_tail", ot)
-                got[ot] = m.eval_batch(toks)
-            m.set_option("o_tail", 1)
-            bad = [i for i in range(len(toks)) if not np.array_equal(got[1][i], got[0][i])]
-            assert not bad, (bi, bad[:10], [len(toks[i]) for i in bad[:10]])
-            assert np.all(np.isfinite(got[1]))
-        toks = batches[0][:60]
-        layers = {}
-        for ot in (1, 0):
-            m.set_option("o_tail", ot)
-            layers[ot] = m.debug_layers(toks)
-        m.set_option("o_tail", 1)
-        for a, b, name in zip(layers[1], layers[0], ("X", "q", "d")):
-            assert np.array_equal(a, b), name
-    finally:
-        m.close()
-
-
-def test_ln_on_read_bitwise(model_dir):
-    """LayerNorm on read (option ln_read; default 0, measured slower): small Q4_0 batches (<= 512
-    padded rows) run the O and FFN-down LayerNorms inside the kernel that reads
-    their output (FFN-up's A rows, the next layer's QKV A rows, the pooling)
-    instead of as passes of their own: the embeddings are bitwise those of the
-    LayerNorm passes, through the fused small QKV + attention kernel (<= 64
-    tokens) and the K-split QKV GEMM (65..128), alone and in small batches,
-    with 2 x n_layer launches fewer per call.  Reference: bert.cpp:944-962,
-    :973-992 (ggml_norm after the residual adds)."""
-    p, _ = get_model(model_dir, "minilm", "q4_0")
-    m = bertlib.BertModel(p)
-    try:
-        assert m.get_option("ln_read") == 0
-        n_layer = m.hparams[5]
-        rng = np.random.default_rng(5)
-        batches = [[sentence(300 + n, n, 30522)] for n in (2, 16, 33, 64, 65, 100, 128)]
-        batches += [[sentence(400 + i, int(n), 30522) for i, n in enumerate(rng.integers(2, 65, 7))],
-                    [sentence(500 + i, int(n), 30522) for i, n in enumerate(rng.integers(2, 129, 4))]]
-        for toks in batches:
-            got, launches = {}, {}
-            for lr in (1, 0):
-                m.set_option("ln_read", lr)
-                got[lr] = m.eval_batch(toks)
-                m.profile(True)
-                m.eval_batch(toks)
-                launches[lr] = sum(c for _, c in m.profile_read().values())
-                m.profile(False)
-            m.set_option("ln_read", 0)
-            lens = [len(t) for t in toks]
-            assert np.array_equal(got[1], got[0]), lens
-            assert np.all(np.isfinite(got[1])), lens
-            assert launches[0] - launches[1] == 2 * n_layer, (lens, launches)
-            m.set_option("ln_read", 1)
-            assert np.array_equal(m.eval(toks[0]), got[1][0]), lens  # bert_eval: the same small path
-            m.set_option("ln_read", 0)
-    finally:
-        m.close()
-
-
 @pytest.mark.parametrize("shape,ftype,n_layer,vocab", [("e5-base", "f16", 1, 250002), ("bge-large", "q4_1", 2, 30522)])
 def test_long_attention_head_dim_64_mixed_lengths(shape, ftype, n_layer, vocab, model_dir):
     """Head dim 64 on the unfused pair (option unfused) with sentences of
