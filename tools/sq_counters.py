@@ -2,7 +2,12 @@
 "Issue floors").  Reads two rocprofv3 --pmc pass directories over bench.py
 (one row group) and the same round's kernel-trace stats for the wall time:
 
-  python3 tools/sq_counters.py <cycles pass dir> <instructions pass dir> <kernel_stats.csv> <out.json> <source>
+  python3 tools/sq_counters.py <cycles pass dir> <instructions pass dir> <kernel_stats.csv | bench.json> <out.json> <source>
+
+Round 6: o-proj and FFN-down both run i8_ln384_kernel (int8 O by default), so
+its dispatches are dealt out in dispatch order (o, down in every layer; one row
+group) and the wall times come from the bench line's per-name event times when
+a bench JSON is given (rocprof's stats merge the two).
 
 SQ_WAVE_CYCLES and the disjoint SQ_WAIT_ANY / SQ_WAIT_INST_ANY /
 SQ_ACTIVE_INST_ANY buckets give the share of wave cycles parked, stalled at
@@ -18,14 +23,17 @@ import json
 import os
 import sys
 
-KERNELS = [("qkv_attention_pc_kernel", "qkv_attention (qkv_attention_pc_kernel)"),
-           ("gemm_kernel", "gemm_o_ln (gemm_kernel split-fp16)"),
-           ("i8_up_gelu_kernel", "gemm_up_gelu (i8_up_gelu_kernel)"),
-           ("i8_ln384_kernel", "gemm_down_ln (i8_ln384_kernel)")]
+# (symbol fragment, label, bench.py kernel name)
+KERNELS = [("qkv_attention_pc_kernel", "qkv_attention (qkv_attention_pc_kernel)", "qkv_attention"),
+           ("gemm_kernel", "gemm_o_ln (gemm_kernel split-fp16)", "gemm_o_ln"),
+           ("i8_up_gelu_kernel", "gemm_up_gelu (i8_up_gelu_kernel)", "gemm_up_gelu"),
+           ("i8_ln384_kernel", "gemm_down_ln (i8_ln384_kernel)", "gemm_down_ln")]
+O_I8 = "gemm_o_ln (i8_ln384_kernel, int8)"
+SHARED = "i8_ln384_kernel"  # o-proj (even dispatches) and FFN-down (odd) when O is int8
 
 
 def label(name):
-    for k, v in KERNELS:
+    for k, v, _ in KERNELS:
         if k in name:
             return v
     return None
@@ -40,18 +48,36 @@ def per_dispatch(root):
                 k = label(row["Kernel_Name"])
                 if k:
                     vals[k][(row["Counter_Name"], row.get("Dispatch_Id", ""))] += float(row["Counter_Value"])
+    split_o = "gemm_o_ln (gemm_kernel split-fp16)" not in vals
     out = {}
     for k, d in vals.items():
-        per = collections.defaultdict(list)
-        for (c, _), v in d.items():
-            per[c].append(v)
-        out[k] = {c: sum(v) / len(v) for c, v in per.items()}
+        groups = {k: d}
+        if split_o and SHARED in k:  # dispatches in order: o, down, o, down, ...
+            ids = sorted({i for _, i in d}, key=lambda x: int(x) if str(x).isdigit() else 0)
+            rank = {i: n for n, i in enumerate(ids)}
+            groups = {O_I8: {key: v for key, v in d.items() if rank[key[1]] % 2 == 0},
+                      k: {key: v for key, v in d.items() if rank[key[1]] % 2 == 1}}
+        for gk, gd in groups.items():
+            per = collections.defaultdict(list)
+            for (c, _), v in gd.items():
+                per[c].append(v)
+            out[gk] = {c: sum(v) / len(v) for c, v in per.items()}
     return out
 
 
-def walls(stats_csv):
+def walls(src):
+    """wall us per label: a bench.py JSON line (per-name event times) or a rocprof kernel-stats CSV"""
     w = {}
-    with open(stats_csv) as fh:
+    if src.endswith(".json"):
+        with open(src) as fh:
+            kern = json.loads(fh.read().strip().splitlines()[-1])["kernels"]
+        for _, v, name in KERNELS:
+            if name in kern:
+                w[v] = kern[name]["avg_us"]
+        if "gemm_o_ln" in kern:
+            w[O_I8] = kern["gemm_o_ln"]["avg_us"]
+        return w
+    with open(src) as fh:
         for row in csv.DictReader(fh):
             k = label(row["Name"])
             if k and k not in w:
@@ -62,7 +88,7 @@ def walls(stats_csv):
 def main(cyc_dir, ins_dir, stats_csv, out, source):
     a, b, w = per_dispatch(cyc_dir), per_dispatch(ins_dir), walls(stats_csv)
     res = {}
-    for _, k in KERNELS:
+    for k in [v for _, v, _ in KERNELS] + [O_I8]:
         if k not in a or k not in b or k not in w:
             continue
         c = {**a[k], **b[k]}
