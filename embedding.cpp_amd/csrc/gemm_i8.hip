@@ -43,6 +43,7 @@ namespace bertamd {
 #ifndef I8_UP_AHEAD
 #define I8_UP_AHEAD 3  // weight blocks in flight (i8_core.h I8Pipe)
 #endif
+constexpr int I8_UP_MAX_N = 4096;  // FFN-up features staged in LDS (n_intermediate: 1536 / 3072 / 4096)
 
 
 // ---------------------------------------------------------------------------
@@ -58,10 +59,14 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
     using C = I8Chunk<BM, wt_q41(WT), WT == W_Q4_1B>;
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ __attribute__((aligned(16))) uint16_t gtab[GELU_FLAT_LDS];
+    // the bias, read by every tile's epilogue: from LDS there (from global memory
+    // each epilogue waited out an L2 round trip after the main loop)
+    __shared__ __attribute__((aligned(16))) float bias_s[I8_UP_MAX_N];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     if (I8_PRIO && wv >= NWV / 2) __builtin_amdgcn_s_setprio(1);
     const int nflat8 = (0x8000 + g.gelu.neg_n + 1 + 7) / 8;
     for (int i = tid; i < nflat8; i += NT) ((uint4 *)gtab)[i] = ((const uint4 *)g.gelu.full)[i];
+    for (int i = tid; i < g.N / 4; i += NT) ((float4v *)bias_s)[i] = ((const float4v *)g.bias)[i];
     const float xlo = h2f((uint16_t)(0x8000 | g.gelu.neg_n));
     const int nwg = n_mtiles * n_ntiles;
     const int fw = F * wv, tw = 0;
@@ -95,7 +100,7 @@ __global__ __launch_bounds__(NWV * 64) void i8_up_gelu_kernel(GemmArgs g, int n_
             float bias[16];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const float4v b4 = *(const float4v *)(g.bias + col + 4 * q);
+                const float4v b4 = *(const float4v *)(bias_s + col + 4 * q);
 #pragma unroll
                 for (int j = 0; j < 4; j++) bias[4 * q + j] = b4[j];
             }
@@ -151,10 +156,17 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
     __shared__ __attribute__((aligned(16))) char smem[2 * C::BYTES];
     __shared__ double red[2][NWV][BM];
     __shared__ __attribute__((aligned(16))) float xs[BM * NCOL];
+    // b, LN weight and LN bias, read by every tile's epilogue: from LDS there
+    // (from global memory each epilogue phase waited out an L2 round trip)
+    __shared__ __attribute__((aligned(16))) float lnp[3][NCOL];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l32 = lane & 31, hh = lane >> 5;
     const int ft0 = wv;
     const int col = 32 * ft0 + 16 * hh;
     if ((int)blockIdx.x >= n_mtiles) return;
+    if (tid < 3 * NCOL / 4) {
+        const int v = tid / (NCOL / 4), i = tid - v * (NCOL / 4);
+        ((float4v *)lnp[v])[i] = ((const float4v *)(v == 0 ? g.bias : v == 1 ? g.ln_w : g.ln_b))[i];
+    }
     if (I8_PRIO && wv >= 2 * NWV / 3) __builtin_amdgcn_s_setprio(1);  // (3 waves per SIMD: the youngest)
     int64_t m0n = (int64_t)xcd_linear(blockIdx.x, n_mtiles) * BM;
     I8Pipe<WT, NT, BM, F, I8_LN_AHEAD> pp;
@@ -219,7 +231,7 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
                 const float4v x4 = *(const float4v *)(xs + 4 * i8_xs_chunk(r, (col >> 2) + qq));
-                const float4v b4 = *(const float4v *)(g.bias + col + 4 * qq);
+                const float4v b4 = *(const float4v *)(lnp[0] + col + 4 * qq);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const float v = (b4[j] + acc[0][t][4 * qq + j]) + x4[j];
@@ -264,8 +276,8 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
             float y[16];
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
-                const float4v w4 = *(const float4v *)(g.ln_w + col + 4 * qq);
-                const float4v b4 = *(const float4v *)(g.ln_b + col + 4 * qq);
+                const float4v w4 = *(const float4v *)(lnp[1] + col + 4 * qq);
+                const float4v b4 = *(const float4v *)(lnp[2] + col + 4 * qq);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     float z = acc[0][t][4 * qq + j] * scale;
@@ -810,7 +822,7 @@ bool i8_gemm_supported(int epi, int N, int K) {
 template <int WT>
 static hipError_t i8_gemm_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s) {
     if (epi == EPI_GELU_ACT) {
-        if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS) return hipErrorInvalidValue;
+        if (0x8000 + a.gelu.neg_n + 1 > GELU_FLAT_LDS || a.N > I8_UP_MAX_N) return hipErrorInvalidValue;
         constexpr int NWV = I8_UP_WAVES, F = I8_UP_F, T = I8_UP_T;
         if (a.N % (32 * NWV * F) || Mpad % (32 * T)) return hipErrorInvalidValue;
         const int mt = Mpad / (32 * T), nt = a.N / (32 * NWV * F);
