@@ -475,24 +475,24 @@ struct I8ResRing {
     int4v wf[4][F];
     uint2 wr[F];
     float4v wdr[F], wmr[F];
+    // Every load is unconditional (a block / chunk past the end reloads the
+    // last one, and the caller drops it), so the compiler's waits stay exact
+    // vmcnt counts: behind a conditional load the control-flow merge made it
+    // wait for vmcnt(0) — for the refill just issued — before the next block.
     __device__ __forceinline__ void wload(const GemmArgs &g, int slot, int ft0, int b) {
-        const int nkb = g.K >> 5;
-        if (b < nkb) {
+        const int nkb = g.K >> 5, bb = b < nkb ? b : nkb - 1;
 #pragma unroll
-            for (int f = 0; f < F; f++) wf[slot][f] = i8_wq(g.Wi, nkb, ft0 + f, b);
-        }
+        for (int f = 0; f < F; f++) wf[slot][f] = i8_wq(g.Wi, nkb, ft0 + f, bb);
     }
     __device__ __forceinline__ void sload(const GemmArgs &g, int ft0, int c) {  // weight scales of chunk c (4 blocks)
-        const int nkb = g.K >> 5, nch = g.K / I8_KC, lane = threadIdx.x & 63;
-        if (c < nch) {
+        const int nkb = g.K >> 5, nch = g.K / I8_KC, lane = threadIdx.x & 63, cc = c < nch ? c : nch - 1;
 #pragma unroll
-            for (int f = 0; f < F; f++) {
-                if constexpr (wt_q41(WT)) {
-                    wdr[f] = i8_wvec(g.Wi.d, nkb, ft0 + f, c);
-                    wmr[f] = i8_wvec(g.Wi.m, nkb, ft0 + f, c);
-                } else {
-                    wr[f] = ((const uint2 *)g.Wi.dh)[((int64_t)(ft0 + f) * (nkb >> 2) + c) * 32 + (lane & 31)];
-                }
+        for (int f = 0; f < F; f++) {
+            if constexpr (wt_q41(WT)) {
+                wdr[f] = i8_wvec(g.Wi.d, nkb, ft0 + f, cc);
+                wmr[f] = i8_wvec(g.Wi.m, nkb, ft0 + f, cc);
+            } else {
+                wr[f] = ((const uint2 *)g.Wi.dh)[((int64_t)(ft0 + f) * (nkb >> 2) + cc) * 32 + (lane & 31)];
             }
         }
     }
@@ -535,8 +535,8 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
         const bool last = c + 1 == nch;
         const char *buf = apanel + c * C::BYTES;
         wscale_use();
-        if (!last) ring.sload(g, ft0, c + 1);
-        else if (ftn >= 0) ring.sload(g, ftn, 0);
+        // the next chunk's scales, or the next f-tile's first (none: f-tile ft0's again, dropped)
+        ring.sload(g, last && ftn >= 0 ? ftn : ft0, last ? 0 : c + 1);
         I8AOps<T> a0, a1;
         i8_aops<WT, BM, T, 0>(a0, buf, tt0);
         // block b0 + j + A into slot (j + A) & 3; past the f-tile's last block,
@@ -544,8 +544,8 @@ __device__ __forceinline__ void i8_resident_mainloop(const GemmArgs &g, const ch
         constexpr int A = AH;
         auto refill = [&](int j) {
             const int b = b0 + j + A;
-            if (b < 4 * nch) ring.wload(g, (j + A) & 3, ft0, b);
-            else if (ftn >= 0) ring.wload(g, (j + A) & 3, ftn, b - 4 * nch);
+            const bool nx = b >= 4 * nch;
+            ring.wload(g, (j + A) & 3, nx && ftn >= 0 ? ftn : ft0, nx ? b - 4 * nch : b);
         };
         i8_block<WT, BM, F, T, 0, true>(buf, tt0, ring.wf[0], ws, wd, wm, a0, a1, acc);
         refill(0);
