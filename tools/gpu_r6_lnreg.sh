@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 6: the int8 LN kernel's overlap with register-staged residual pieces
+# (exact vmcnt waits), for FFN-down and o-proj (build) or FFN-down only —
+# bitwise against the previous library, then alternating headline runs (3 each).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+timeout -k 10 300 python3 tools/bitwise_libs.py build/ab/head/libbert.so build/libbert.so build/ab/ppc_down_only/libbert.so > gpurun_out/lnreg_bitwise.log 2>&1 || { tail -20 gpurun_out/lnreg_bitwise.log; exit 1; }
+tail -3 gpurun_out/lnreg_bitwise.log
+REPS=3 bash tools/lib_ab.sh "--steps 20 --warmup 5 --ragged-steps 5" build/libbert.so build/ab/ppc_down_only/libbert.so build/ab/head/libbert.so
