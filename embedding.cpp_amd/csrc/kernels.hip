@@ -1738,14 +1738,9 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
     constexpr int NK = 128, KST = D + 8, VST = NK + 4, E = 384, NKB = E / 32;
     using C = I8Chunk<BM, false>;
     constexpr int SLOT = (4 * NK * KST + 2 * D * VST) * 2;  // Qh Ql Kh Kl, Vh Vl of one head, bytes
-    // one LDS block: the attention tiles, the exp table, the panel — the table's
-    // address then fits the DS offset field, so a lookup's address is one shift
-    // of the fp16 pattern
-    static_assert(SLOT % 16 == 0 && SLOT + 2 < 65536, "exp table offset");
-    __shared__ __attribute__((aligned(16))) char lds[SLOT + EXP_TABLE_LDS * 2 + (E / I8_KC) * C::BYTES];
-    char *const tiles = lds;
-    uint16_t *const etab = (uint16_t *)(lds + SLOT);
-    char *const apanel = lds + SLOT + EXP_TABLE_LDS * 2;
+    __shared__ __attribute__((aligned(16))) char apanel[(E / I8_KC) * C::BYTES];
+    __shared__ __attribute__((aligned(16))) char tiles[SLOT];
+    __shared__ __attribute__((aligned(16))) uint16_t etab[EXP_TABLE_LDS];
     __shared__ int qtab[PK ? 4 : 1][4];     // query block -> {first tile row of its sentence, length, first query, vs}
     __shared__ uint8_t vslot[PK ? NK : 1];  // tile row -> V^T key slot
     const int s0 = PK ? a.tiles[2 * blockIdx.x] : (int)blockIdx.x;
@@ -1924,32 +1919,24 @@ __global__ __launch_bounds__(QKPC_NW * 64) void qkv_attention_pc_kernel(GemmArgs
                 }
                 mx = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;
                 const float2v mx2 = {mx, mx}, sc2 = {a.scale, a.scale};
-                const ushort2v en2 = {(uint16_t)eneg, (uint16_t)eneg};
                 // pass 2: p = exp_tab[fp16(s - max)], the exact integer sum of p * 2^24, and
-                // V.P over the key tiles in order.  Two scores at a time: one packed
-                // fp16 conversion and one packed clamp; the table sits at a fixed LDS
-                // offset (pos_n == 1, checked by the launcher), so each lookup address
-                // is one shift of a 16-bit half (4 VALU per pair instead of 6)
+                // V.P over the key tiles in order
                 o[0] = float16v{};
 #pragma unroll
                 for (int kt = 0; kt < 4; kt++) {
                     if (kt >= nkt) continue;
                     half8 ph[2];
-                    ushort2v hm[8];
 #pragma unroll
                     for (int j = 0; j < 16; j += 2) {
                         const float2v d2 = mx2 - float2v{Sk[kt][j], Sk[kt][j + 1]} * sc2;
-                        hm[j >> 1] = __builtin_elementwise_min(
-                            __builtin_bit_cast(ushort2v, __builtin_convertvector(d2, half2v)), en2);
-                    }
-                    uint16_t pb[16];
+                        uint16_t pb[2];
 #pragma unroll
-                    for (int i = 0; i < 16; i++) pb[i] = etab[1 + (uint32_t)hm[i >> 1][i & 1]];
-#pragma unroll
-                    for (int i = 0; i < 16; i++) ph[i >> 3][i & 7] = __builtin_bit_cast(_Float16, pb[i]);
-#pragma unroll
-                    for (int j = 0; j < 16; j += 2) {
-                        const float2v pp = float2v{h2f(pb[j]), h2f(pb[j + 1])} * float2v{16777216.0f, 16777216.0f};
+                        for (int e = 0; e < 2; e++) {
+                            const uint32_t hm = f2h(d2[e]);
+                            pb[e] = etab[epos + min(hm, (uint32_t)eneg)];
+                            ph[(j + e) >> 3][(j + e) & 7] = __builtin_bit_cast(_Float16, pb[e]);
+                        }
+                        const float2v pp = float2v{h2f(pb[0]), h2f(pb[1])} * float2v{16777216.0f, 16777216.0f};
                         sum += (uint32_t)pp[0] + (uint32_t)pp[1];
                     }
                     attn_pv_h<D, 1>(o, Vh, Vl, VST, vs + 32 * kt, r, hh, ph, 0);
@@ -1970,7 +1957,6 @@ static hipError_t qkv_attn_t(const GemmArgs &g, const AttnArgs &a, int n_blocks,
     const bool pk = a.tiles != nullptr;
     if constexpr (D == 32 && WT == W_Q4_0) {
         if (ntw == 0) {  // producer / consumer waves (qkv_attention_pc_kernel; g.Wi: int8 QKV weights)
-            if (a.expt.pos_n != 1) return hipErrorInvalidValue;  // the consumers' fixed table offset
             if (pk)
                 hipLaunchKernelGGL((qkv_attention_pc_kernel<true>), dim3(n_blocks), dim3(QKPC_NW * 64), 0, s, g, a);
             else

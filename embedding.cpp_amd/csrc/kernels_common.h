@@ -15,7 +15,6 @@ typedef float float16v __attribute__((ext_vector_type(16)));
 typedef _Float16 half4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));  // 16 raw bytes as a register vector
 typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));  // two fp16 bit patterns
 
 // Development phase stamps (tools/phase_stamps.hip): compiled out of the
 // library; with -DPHASE_STAMPS lane 0 of waves 0 and NW - 1 of each
