@@ -184,13 +184,12 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
         int j0;
         const int off = piece_off(k, j0);
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(xt + off),
-                                         (__attribute__((address_space(3))) void *)(xs + 4 * j0), 16, 0,
-                                         I8_NT ? 2 : 0);  // aux 2: nt
+                                         (__attribute__((address_space(3))) void *)(xs + 4 * j0), 16, 0, 0);
     };
     auto store_out = [&](float *xt, int k) {
         int j0;
         const int off = piece_off(k, j0);
-        i8_st_stream((float4v *)(xt + off), *(const float4v *)(xs + 4 * (j0 + lane)));
+        *(float4v *)(xt + off) = *(const float4v *)(xs + 4 * (j0 + lane));
     };
     int64_t mprev = -1;
     for (int tile = blockIdx.x, it = 0; tile < n_mtiles; tile += gridDim.x, it++) {

@@ -72,22 +72,6 @@ struct I8Items {
     uint16_t d16[IT];    // Q8_0
 };
 
-// A/B: streamed activations (A chunks in, Q8 rows out) with the nontemporal
-// cache policy, so the weights each workgroup re-reads every tile stay in L2
-#ifndef I8_NT
-#define I8_NT 0
-#endif
-template <typename T>
-__device__ __forceinline__ T i8_ld_stream(const T *p) {
-    if constexpr (I8_NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <typename T>
-__device__ __forceinline__ void i8_st_stream(T *p, T v) {
-    if constexpr (I8_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
 template <int WT, int BM, int NT>
 __device__ __forceinline__ void i8_stage_load(I8Items<(4 * BM + NT - 1) / NT> &st, const ActPtr &A, int K, int64_t m0,
                                               int k0) {
@@ -101,13 +85,13 @@ __device__ __forceinline__ void i8_stage_load(I8Items<(4 * BM + NT - 1) / NT> &s
             const int r = item >> 2, bb = item & 3;
             const int64_t row = m0 + r;
             const int4v *p = (const int4v *)((const int8_t *)A.q + row * K + k0 + 32 * bb);
-            st.q0[it] = i8_ld_stream(p);
-            st.q1[it] = i8_ld_stream(p + 1);
+            st.q0[it] = p[0];
+            st.q1[it] = p[1];
             const int64_t bi = row * (K >> 5) + (k0 >> 5) + bb;
             if constexpr (WT == W_Q4_0)
-                st.d16[it] = i8_ld_stream((const uint16_t *)A.d + bi);
+                st.d16[it] = ((const uint16_t *)A.d)[bi];
             else
-                st.d[it] = i8_ld_stream((const float *)A.d + bi);
+                st.d[it] = ((const float *)A.d)[bi];
         }
     }
 }
@@ -455,12 +439,12 @@ __device__ __forceinline__ void i8_store_q8_half(const ActPtr &out, int64_t ld, 
     pk.y = q8_pack4(y[4], y[5], y[6], y[7], id);
     pk.z = q8_pack4(y[8], y[9], y[10], y[11], id);
     pk.w = q8_pack4(y[12], y[13], y[14], y[15], id);
-    i8_st_stream((u32x4v *)((int8_t *)out.q + row * ld + 32 * blk + 16 * hh), __builtin_bit_cast(u32x4v, pk));
+    *(uint4 *)((int8_t *)out.q + row * ld + 32 * blk + 16 * hh) = pk;
     if (hh == 0) {
         if constexpr (WT == W_Q4_0)
-            i8_st_stream((uint16_t *)out.d + row * (ld >> 5) + blk, f2h(d));
+            ((uint16_t *)out.d)[row * (ld >> 5) + blk] = f2h(d);
         else
-            i8_st_stream((float *)out.d + row * (ld >> 5) + blk, d);
+            ((float *)out.d)[row * (ld >> 5) + blk] = d;
     }
 }
 
