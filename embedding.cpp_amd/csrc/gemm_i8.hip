@@ -148,7 +148,7 @@ __device__ __forceinline__ int i8_xs_chunk(int r, int c) { return r * 96 + (c ^ 
 #define I8_LN_PIPE 1  // i8_block's two-tile software pipeline in this kernel's main loop
 #endif
 
-template <int WT, bool OV = I8_LN_OV>
+template <int WT, bool NTX, bool OV = I8_LN_OV>
 __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles) {
     constexpr int NT = 768, BM = 64, F = 1, T = 2, NCOL = 384, NWV = 12;
     constexpr int XCH = BM * NCOL / 4;  // 16-byte chunks of the residual tile
@@ -189,7 +189,9 @@ __global__ __launch_bounds__(768) void i8_ln384_kernel(GemmArgs g, int n_mtiles)
     auto store_out = [&](float *xt, int k) {
         int j0;
         const int off = piece_off(k, j0);
-        *(float4v *)(xt + off) = *(const float4v *)(xs + 4 * (j0 + lane));
+        const float4v v = *(const float4v *)(xs + 4 * (j0 + lane));
+        if constexpr (NTX) __builtin_nontemporal_store(v, (float4v *)(xt + off));
+        else *(float4v *)(xt + off) = v;
     };
     int64_t mprev = -1;
     for (int tile = blockIdx.x, it = 0; tile < n_mtiles; tile += gridDim.x, it++) {
@@ -829,7 +831,10 @@ static hipError_t i8_gemm_t(int epi, const GemmArgs &a, int Mpad, hipStream_t s)
         hipLaunchKernelGGL((i8_up_gelu_kernel<WT, NWV, F, T>), dim3(persistent_grid(mt * nt)), dim3(NWV * 64), 0, s, a, mt, nt);
     } else if (epi == EPI_LN) {
         const int mt = Mpad / 64;
-        hipLaunchKernelGGL((i8_ln384_kernel<WT>), dim3(persistent_grid(mt)), dim3(768), 0, s, a, mt);
+        if (a.nt_x)
+            hipLaunchKernelGGL((i8_ln384_kernel<WT, true>), dim3(persistent_grid(mt)), dim3(768), 0, s, a, mt);
+        else
+            hipLaunchKernelGGL((i8_ln384_kernel<WT, false>), dim3(persistent_grid(mt)), dim3(768), 0, s, a, mt);
     } else if (epi == EPI_RESID) {
         const int mt = Mpad / 64, nt = a.N / 256;
         hipLaunchKernelGGL((i8_resid_kernel<WT>), dim3(persistent_grid(mt * nt)), dim3(512), 0, s, a, mt, nt);

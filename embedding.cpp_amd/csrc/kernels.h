@@ -121,6 +121,11 @@ struct GemmArgs {
     // EPI_LN in launch_gemm_i8_small: leave (b + W.x) + X in X; the caller runs
     // the LayerNorm pass (launch_ln384_rows_i8) as a launch of its own
     int defer_ln = 0;
+    // EPI_LN (i8_ln384_kernel): store the f32 rows X with the nontemporal cache
+    // policy (the next reader is another kernel, which reads them from HBM /
+    // the fabric anyway; without them the weights stay in L2).  Off where the
+    // next reader gains from them being cached (the last layer's X -> pooling)
+    int nt_x = 0;
 };
 
 struct EmbedArgs {

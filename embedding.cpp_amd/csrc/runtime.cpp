@@ -295,6 +295,9 @@ struct bert_ctx {
     // one-sentence call measured 327 us eager, 332 us replayed — the device's
     // ~4.5 us per dependent kernel bounds it, not the host's launches)
     int graph_seqs = 0;
+    // the 384-wide LN kernel stores X with the nontemporal policy (GemmArgs
+    // nt_x; not the last layer's, which pooling reads next): 1 (default) / 0
+    int nt_x = 1;
     // small batches (<= 512 padded rows, every sentence <= 128 tokens; Q4_0 at
     // n_embd 384, head dim 32, int8 QKV): each head's QKV and attention in one
     // kernel (kernels.hip qkv_attention_small_kernel; bitwise the unfused pair)
@@ -834,6 +837,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         // small batches: the int8 O + LN is the 32-row residual GEMM, then the
         // LayerNorm pass as a launch of its own (counted as one in the profile)
         o.defer_ln = small;
+        o.nt_x = ctx->nt_x;
         if (ctx->i8_o) {
             o.Wi = L.o8;
             if (E == 384) {
@@ -872,6 +876,7 @@ bool run_layer(bert_ctx *ctx, Replica &R, Lane &ln, int il, int64_t row0, int64_
         dn.ln_b = L.ln2_b;
         dn.eps = hp.eps;
         dn.defer_ln = small;  // (as O)
+        dn.nt_x = ctx->nt_x && il + 1 < ctx->hp.n_layer;  // the last layer's X: pooling reads it next
         if (ctx->i8_up) {
             u.Wi = L.up8;
             LAUNCH_OK("gemm_up_gelu", gemm_i8(EPI_GELU_ACT, u));
@@ -1312,6 +1317,8 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
         ctx->unfused = value != 0;
     } else if (k == "small_qkva") {
         ctx->small_qkva = value != 0;
+    } else if (k == "nt_x") {
+        ctx->nt_x = value != 0;
     } else if (k == "small_rows" || k == "graph_seqs") {
         if (need(value >= 0, "must be >= 0")) return -2;
         (k == "small_rows" ? ctx->small_rows : ctx->graph_seqs) = value;
@@ -1334,7 +1341,7 @@ int apply_option(bert_ctx *ctx, const std::string &k, int32_t value) {
 // too.  Returns false with the error set.
 bool parse_load_options(bert_ctx *ctx, const char *opts, std::string &i8_spec) {
     static const char *keys[] = {"i8", "qkva_ntw", "q41bf", "split", "pack", "fuse_min", "unfused", "small_rows", "graph_seqs",
-                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows", "emb_raw"};
+                                 "small_qkva", "encode_lanes", "encode_merge", "encode_merge_rows", "emb_raw", "nt_x"};
     std::vector<std::pair<std::string, std::string>> kv;
     for (const char *k : keys) {
         std::string env = "BERT_AMD_" + std::string(k);
@@ -2371,7 +2378,7 @@ int32_t bert_amd_get_option(bert_ctx *ctx, const char *key, int32_t *value) {
         {"encode_lanes", ctx->encode_lanes}, {"encode_merge", ctx->encode_merge},
         {"encode_merge_rows", ctx->encode_merge_rows}, {"qkva_ntw", ctx->qkva_ntw},
         {"i8_qkv", ctx->i8_qkv}, {"i8_up", ctx->i8_up}, {"i8_o", ctx->i8_o}, {"i8_down", ctx->i8_down},
-        {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw},
+        {"q41bf", ctx->q41bf}, {"emb_raw", ctx->emb_raw}, {"nt_x", ctx->nt_x},
         // resolved: FFN-up / FFN-down on the bf16 scale products (Q4_1 on the int8 GEMMs)
         {"q41bf_qkv", ctx->wtype == W_Q4_1 && ctx->i8_qkv && q41bf_for(ctx->q41bf, EPI_QKV)},
         {"q41bf_o", ctx->wtype == W_Q4_1 && ctx->i8_o && q41bf_for(ctx->q41bf, ctx->hp.n_embd == 384 ? EPI_LN : EPI_RESID)},

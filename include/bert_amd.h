@@ -139,6 +139,10 @@ BERT_API int64_t bert_amd_workspace_rows(struct bert_ctx *ctx, int32_t slot);
                         sentences all have <= 64 tokens (Q4_0, n_embd 384, head
                         dim 32) run each head's int8 QKV and its attention in one
                         kernel (same results; one launch less per layer)
+     "nt_x" 0 | 1        1 (default): the 384-wide projection + LayerNorm kernel
+                        stores X with the nontemporal cache policy (all but the
+                        last layer's X, which the pooling reads next), so the
+                        weights its tiles re-read stay in L2; 0 plain stores
      "graph_seqs" n >= 0 host batches of at most n sentences (and fewer than
                         fuse_min) replay a captured HIP graph of their launches
                         (default 0: measured no faster)
